@@ -1,0 +1,225 @@
+"""Generate golden vectors by running the REFERENCE itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 OPENBLAS_NUM_THREADS=1 python tests/golden/make_golden.py
+
+The reference (fdeguire03/InteriorPoint-GPU @ /root/reference) is imported
+read-only with an empty ``cvxpy`` stub module (cvxpy is only touched when
+``check_cvxpy=True``).  Its methods are wrapped at run time
+(never edited) to record per-iteration step sizes.  Only inputs and outputs
+are written (``tests/golden/*.npz``); nothing from the reference's source is
+stored.  The GPU box never sees /root/reference -- it receives these files.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "interiorpoint-gpu_amd"))
+sys.modules.setdefault("cvxpy", types.ModuleType("cvxpy"))
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+
+import FunctionManager as RFM  # noqa: E402
+import NewtonSolver as RNS  # noqa: E402
+import NewtonSolverInfeasibleStart as RNSI  # noqa: E402
+from LPSolver import LPSolver as RefLP  # noqa: E402
+from QPSolver import QPSolver as RefQP  # noqa: E402
+from SOCPSolver import SOCPSolver as RefSOCP  # noqa: E402
+
+from ipm355 import problems  # noqa: E402
+
+TRACE = []
+
+
+def _wrap_feasible():
+    orig = RNS.NewtonSolver.backtrack_search
+
+    def rec(self, x, xstep, t, gradf):
+        s = orig(self, x, xstep, t, gradf)
+        TRACE.append(("F", float(s), bool(getattr(self, "phase1_flag", False))))
+        return s
+    RNS.NewtonSolver.backtrack_search = rec
+
+    orig_i = RNSI.NewtonSolverInfeasibleStart.backtrack_search
+
+    def rec_i(self, *a, **k):
+        out = orig_i(self, *a, **k)
+        TRACE.append(("I", float(out[0]), False))
+        return out
+    RNSI.NewtonSolverInfeasibleStart.backtrack_search = rec_i
+
+
+def _pack_list(prefix, arrs, out):
+    out[prefix + "_count"] = np.array(len(arrs))
+    for i, a in enumerate(arrs):
+        out[f"{prefix}_{i}"] = np.asarray(a)
+
+
+def run_solve(name, cls, kwargs, solve_kwargs=None, rand_seed=None):
+    TRACE.clear()
+    if rand_seed is not None:
+        np.random.seed(rand_seed)
+    out = {}
+    for k, v in kwargs.items():        # snapshot inputs BEFORE the reference mutates them (Q8, Q16)
+        if v is None:
+            continue
+        if isinstance(v, list):
+            _pack_list("in_" + k, [np.array(a, copy=True) for a in v], out)
+        else:
+            out["in_" + k] = np.array(v, copy=True)
+    def _cp(a):
+        return np.array(a, copy=True) if isinstance(a, np.ndarray) else a
+    kw = {k: ([_cp(a) for a in v] if isinstance(v, list) else _cp(v)) for k, v in kwargs.items()}
+    kw.setdefault("check_cvxpy", False)
+    kw.setdefault("suppress_print", True)
+    solver = cls(**kw)
+    x_init = np.array(solver.x, copy=True)
+    val = solver.solve(**(solve_kwargs or {}))
+    out["x_init"] = x_init
+    out["value"] = np.array(val)
+    out["xstar"] = np.asarray(solver.xstar)
+    out["inner_iters"] = np.array(solver.inner_iters)
+    out["outer_iters"] = np.array(solver.outer_iters)
+    ph = getattr(solver, "phase1_solver", None)
+    out["phase1_inner_iters"] = np.array(getattr(ph, "inner_iters", []) if ph is not None and hasattr(ph, "inner_iters") else [])
+    out["trace_kind"] = np.array([t[0] for t in TRACE])
+    out["trace_step"] = np.array([t[1] for t in TRACE])
+    out["trace_phase1"] = np.array([t[2] for t in TRACE])
+    out["use_backup"] = np.array(bool(getattr(solver.ns, "use_backup", False)))
+    out["phase1_use_backup"] = np.array(bool(getattr(getattr(ph, "phase1_ns", None), "use_backup", False)))
+    out["solve_kwargs"] = np.array(repr(solve_kwargs or {}))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(f"{name}: value={val!r} inner={solver.inner_iters} steps={len(TRACE)}")
+
+
+def fm_kats():
+    """Per-function values at fixed (x, t), plus the stale-slack values after
+    update_x(x2, update_slacks=False) (quirk Q2)."""
+    rng = np.random.default_rng(7)
+    n, m = 12, 5
+    C = rng.uniform(-1, 1, (m, n)); d = rng.uniform(1, 2, m); c = rng.normal(size=n)
+    x = rng.uniform(-0.2, 0.2, n); x2 = x + 0.05 * rng.normal(size=n)
+    Pp = rng.normal(size=(n, n)); P = Pp.T @ Pp + np.eye(n); q = rng.normal(size=n)
+    lb, ub = np.array(-1.0), np.array(1.0)
+    t = 3.7
+    out = dict(C=C, d=d, c=c, x=x, x2=x2, P=P, q=q, lb=lb, ub=ub, t=np.array(t))
+
+    def grab(tag, fm, xv, xs):
+        fm.update_x(xv)
+        fm.update_t(t)
+        out[tag + "_slacks"] = np.array(fm.slacks)
+        out[tag + "_nobj"] = np.array(fm.newton_objective())
+        out[tag + "_grad"] = np.array(fm.gradient())
+        out[tag + "_hess"] = np.array(fm.hessian())
+        fm.update_x(xs, update_slacks=False)
+        out[tag + "_stale_nobj"] = np.array(fm.newton_objective())
+        out[tag + "_stale_grad"] = np.array(fm.gradient())
+
+    grab("lp", RFM.FunctionManagerLP(c=c, C=C, d=d, x0=x.copy(), lower_bound=lb, upper_bound=ub, t=1), x.copy(), x2.copy())
+    grab("qp", RFM.FunctionManagerQP(P=P, q=q, C=C, d=d, x0=x.copy(), lower_bound=lb, upper_bound=ub, t=1), x.copy(), x2.copy())
+    fm = RFM.FunctionManagerLP(c=c, C=None, d=None, x0=x.copy(), lower_bound=lb, upper_bound=ub, t=1, try_diag=True)
+    fm.update_x(x.copy()); fm.update_t(t)
+    out["lpdiag_grad"] = np.array(fm.gradient()); out["lpdiag_hess"] = np.array(fm.hessian())
+    out["lpdiag_ihess"] = np.array(fm.inv_hessian())
+    # phase 1 (infeasible x so s0 > 1)
+    xi = rng.uniform(-3, 3, n)
+    out["xi"] = xi
+    fm = RFM.FunctionManagerPhase1(C=C, d=d, x0=xi.copy(), lower_bound=lb, upper_bound=ub, t=1)
+    out["ph1_s0"] = np.array(fm.s)
+    xt = np.append(xi, fm.s)
+    grab("ph1", fm, xt.copy(), xt + 0.01)
+    # SOCP: 3 dense cones + 1 diagonal cone, bounds
+    K, mi = 3, 4
+    A = [rng.normal(size=(mi, n)) for _ in range(K)] + [np.diag(rng.uniform(0.5, 1.0, n))]
+    b = [rng.normal(size=mi) for _ in range(K)] + [rng.normal(size=n) * 0.1]
+    cc = [rng.normal(size=n) * 0.1 for _ in range(K + 1)]
+    x0 = rng.normal(size=n) * 0.1
+    dd = [float(np.linalg.norm((A[i] @ x0) + b[i]) - cc[i] @ x0 + 1) for i in range(K + 1)]
+    _pack_list("socp_A", A, out); _pack_list("socp_b", b, out); _pack_list("socp_c", cc, out)
+    out["socp_d"] = np.array(dd); out["socp_x0"] = x0
+    lbs, ubs = np.array(-5.0), np.array(5.0)
+    Ac = [a.copy() for a in A]
+    Ac[-1] = np.diag(A[-1]).copy()  # the facade's diagonal compression (SOCPSolver.py:285-292)
+    fm = RFM.FunctionManagerSOCP(P=P, q=q, A=Ac, b=b, c=cc, d=dd, x0=x0.copy(), lower_bound=lbs, upper_bound=ubs, t=1)
+    grab("socp", fm, x0.copy(), x0 + 0.01)
+    xs_inf = x0 + rng.normal(size=n) * 3
+    out["socp_xi"] = xs_inf
+    fm = RFM.FunctionManagerSOCPPhase1(A=Ac, b=b, c=cc, d=dd, x0=xs_inf.copy(), lower_bound=lbs, upper_bound=ubs, t=1)
+    out["sph1_s0"] = np.array(fm.s)
+    xt = np.append(xs_inf, fm.s)
+    grab("sph1", fm, xt.copy(), xt + 0.01)
+    np.savez_compressed(os.path.join(HERE, "fm_kats.npz"), **out)
+    print("fm_kats written")
+
+
+def group_lasso():
+    """demo.ipynb cells 26-31: HW5 group lasso as an SOCP; known answer FSTAR."""
+    LAMBDA = 0.02
+    GROUPS = [[0], [1], [2], [3, 4, 5, 6, 7], [8, 9, 10, 11, 12, 13], [14, 15], [16], [17], [18]]
+    X = np.loadtxt(os.path.join(REF, "example_data/X_train.csv"), delimiter=",")
+    X = np.hstack([np.ones(X.shape[0])[:, None], X])
+    Y = np.loadtxt(os.path.join(REF, "example_data/Y_train.csv"), delimiter=",")
+    w = np.sqrt(list(map(len, GROUPS)))[1:]
+    N = X.shape[0]
+    P = np.zeros((27, 27)); P[:19, :19] = 1 / N * X.T @ X
+    q = np.zeros(27); q[:19] = -1 / N * Y.T @ X; q[19:] = LAMBDA * w
+    A, c = [], []
+    for i in range(len(GROUPS) - 1):
+        Ai = np.zeros((27, 27)); ci = np.zeros(27)
+        Ai[GROUPS[i + 1], GROUPS[i + 1]] = 1; ci[i + 19] = 1
+        A.append(Ai); c.append(ci)
+    kw = dict(P=P, q=q, A=[a.copy() for a in A], b=None, c=c, d=None, lower_bound=None, upper_bound=None)
+    run_solve("socp_group_lasso", RefSOCP, kw, rand_seed=0)
+    z = dict(np.load(os.path.join(HERE, "socp_group_lasso.npz")))
+    z["yty_over_2n"] = np.array(Y @ Y / (2 * N))
+    z["fstar"] = np.array(49.9649387126726)
+    z["in_A_dense_count"] = np.array(len(A))
+    for i, a in enumerate(A):
+        z[f"in_A_dense_{i}"] = a
+    np.savez_compressed(os.path.join(HERE, "socp_group_lasso.npz"), **z)
+
+
+def main():
+    _wrap_feasible()
+    fm_kats()
+    run_solve("lp_eq_box", RefLP, dict(problems.lp_eq_box(200, 50, seed=0), update_slacks_every=5))
+    run_solve("lp_ineq_box", RefLP, problems.lp_ineq_box(200, 50, seed=0))
+    run_solve("lp_ineq_box_testkw", RefLP, dict(problems.lp_ineq_box(128, 32, seed=3), **problems.LP_KWARGS))
+    run_solve("qp_ineq_box", RefQP, dict(problems.qp_ineq_box(128, 32, seed=1), **problems.QP_KWARGS))
+    run_solve("qp_ineq_box_256", RefQP, dict(problems.qp_ineq_box(256, 64, seed=2), **problems.QP_KWARGS))
+    # feasible start, no phase 1 (x0 strictly feasible): d = C x_f + 1 with x_f = 0 region
+    pr = problems.qp_ineq_box(96, 24, seed=4)
+    pr["d"] = np.abs(pr["d"]) + 1.0
+    run_solve("qp_feasible", RefQP, dict(pr, **problems.QP_KWARGS))
+    # QP with an equality row + phase 1 (demo.ipynb cell 22 pattern)
+    rng = np.random.default_rng(5)
+    n = 60
+    C = rng.random((25, n)) * rng.binomial(1, 0.3, (25, n))
+    d = rng.integers(1, 30, 25).astype(float)
+    c = rng.integers(1, n, n) - n / 2
+    Aeq = np.hstack((1, np.zeros(n - 1))).reshape(1, -1)
+    run_solve("qp_eq_phase1", RefQP, dict(P=np.eye(n), q=c, A=Aeq, b=np.array([1.0]), C=C, d=d, t0=0.1,
+                                          upper_bound=None, lower_bound=0, mu=15, x0=np.ones(n) * 10))
+    # LP with equality AND inequality constraints (dense infeasible-start Cholesky + phase 1)
+    rng = np.random.default_rng(6)
+    n = 80
+    Aeq = rng.uniform(-2, 2, (20, n)); C = rng.uniform(-2, 2, (10, n)); xf = rng.uniform(-2, 2, n)
+    run_solve("lp_eq_ineq", RefLP, dict(c=rng.uniform(-2, 2, n), A=Aeq, b=Aeq @ xf, C=C, d=C @ xf + 1,
+                                        lower_bound=-3, upper_bound=3, **problems.LP_KWARGS))
+    run_solve("socp_small", RefSOCP, dict(problems.socp_cones(64, 8, 4, seed=0), **problems.SOCP_KWARGS))
+    run_solve("socp_small_eq", RefSOCP, dict(problems.socp_cones(48, 6, 4, seed=1, eq=5), **problems.SOCP_KWARGS))
+    pr = problems.socp_cones(40, 5, 3, seed=2)
+    pr["x0"] = pr["x0"] + 0.7 * np.random.default_rng(9).normal(size=40)  # infeasible -> SOCP phase 1
+    run_solve("socp_phase1", RefSOCP, dict(pr, t0=0.1))
+    group_lasso()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,44 @@
+"""Load golden fixtures (tests/golden/*.npz, written by make_golden.py) back into
+solver kwargs.  Pure data handling -- no reference code is involved."""
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+
+SOLVE_CASES = {
+    "lp_eq_box": "LP", "lp_ineq_box": "LP", "lp_ineq_box_testkw": "LP", "lp_eq_ineq": "LP",
+    "qp_ineq_box": "QP", "qp_ineq_box_256": "QP", "qp_feasible": "QP", "qp_eq_phase1": "QP",
+    "socp_small": "SOCP", "socp_small_eq": "SOCP", "socp_phase1": "SOCP", "socp_group_lasso": "SOCP",
+}
+
+# kwargs that are stored as scalars in the fixture but are not array inputs
+_SCALAR_KW = {"t0", "mu", "epsilon", "alpha", "beta", "max_inner_iters", "max_outer_iters",
+              "update_slacks_every", "lower_bound", "upper_bound"}
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+
+
+def solver_kwargs(z):
+    kw = {}
+    lists = {k[3:-6] for k in z if k.startswith("in_") and k.endswith("_count")}
+    for key in lists:
+        if key == "A_dense":
+            continue
+        cnt = int(z[f"in_{key}_count"])
+        kw[key] = [z[f"in_{key}_{i}"] for i in range(cnt)]
+        kw[key] = [float(v) if np.ndim(v) == 0 else v for v in kw[key]]
+    for k, v in z.items():
+        if not k.startswith("in_") or k.endswith("_count"):
+            continue
+        name = k[3:]
+        if any(name.startswith(l + "_") and name[len(l) + 1:].isdigit() for l in lists):
+            continue
+        if name in _SCALAR_KW and np.ndim(v) == 0:
+            v = v.item()
+        kw[name] = v
+    for b in ("lower_bound", "upper_bound"):
+        kw.setdefault(b, None)
+    return kw

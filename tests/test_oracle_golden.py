@@ -1,0 +1,123 @@
+"""Pin the CPU oracle (oracle/ipm_oracle.py) against the reference's own outputs.
+
+Golden vectors were produced by running the reference itself in the build
+container (tests/golden/make_golden.py).  The oracle must reproduce:
+  * per-function values at fixed (x, t), incl. stale-slack quirks (Q2)   -- <=1e-12 rel
+  * the phase-1 known answers of AutomatedTestsPhaseOne.py:15-220         -- 1e-8 (the KAT's tol)
+  * full solves: identical inner-iteration counts and step-size traces,
+    x* and the objective to 1e-9 rel, and the SOCP group-lasso FSTAR KAT.
+"""
+import numpy as np
+import pytest
+
+from golden_io import SOLVE_CASES, load, solver_kwargs
+from oracle import ipm_oracle as O
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def test_phase1_known_answers():
+    """AutomatedTestsPhaseOne.py:29-39, 60-75, 112-129, 150-170, 210-218 (constants restated)."""
+    G = np.array([[1., 2, 3], [4, 5, 6]]); h = np.array([2., 3])
+    fm = O.Phase1Barrier(C=G, d=h, x0=np.ones(3), t=1)
+    assert fm.s == 13
+    g = fm.gradient()
+    assert np.linalg.norm(g - np.hstack([np.array([1, 2, 3]) / 9 + np.array([4, 5, 6]), -1 / 9])) <= 1e-8
+    H = fm.hessian()
+    hxx = np.array([[1, 2, 3], [2, 4, 6], [3, 6, 9]]) / 81 + np.array([[16, 20, 24], [20, 25, 30], [24, 30, 36]])
+    hxs = (-np.array([1, 2, 3]) / 81 - np.array([4, 5, 6])).reshape(3, 1)
+    assert np.linalg.norm(H - np.block([[hxx, hxs], [hxs.T, np.array([[1 + 1 / 81]])]])) <= 1e-8
+    assert abs(fm.newton_objective() - (13 - np.log(9))) <= 1e-8
+    G = np.array([[-1., -3], [-1, 1], [1, -2], [1, 4]]); h = np.array([-6., 2, -2, 12])
+    fm = O.Phase1Barrier(C=G, d=h, x0=np.ones(2), t=1)
+    assert fm.s == 3
+    gx = np.array([-1, -3]) + np.array([-1, 1]) / 5 + np.array([1, -2]) / 2 + np.array([1, 4]) / 10
+    assert np.linalg.norm(fm.gradient() - np.hstack([gx, -1 / 5 - 1 / 2 - 1 / 10])) <= 1e-8
+    hxx = (np.array([[1, 3], [3, 9]]) + np.array([[1, -1], [-1, 1]]) / 25 + np.array([[1, -2], [-2, 4]]) / 4
+           + np.array([[1, 4], [4, 16]]) / 100)
+    hxs = (-np.array([-1, -3]) - np.array([-1, 1]) / 25 - np.array([1, -2]) / 4 - np.array([1, 4]) / 100).reshape(-1, 1)
+    Ht = np.block([[hxx, hxs], [hxs.T, np.array([[1 + 1 / 25 + 1 / 4 + 1 / 100]])]])
+    assert np.linalg.norm(fm.hessian() - Ht) <= 1e-8
+
+
+def _fm_from_kats(z, tag):
+    lb, ub = z["lb"], z["ub"]
+    if tag == "lp":
+        return O.LPBarrier(c=z["c"], C=z["C"], d=z["d"], x0=z["x"].copy(), lb=lb, ub=ub, t=1), z["x"], z["x2"]
+    if tag == "qp":
+        return O.QPBarrier(P=z["P"], q=z["q"], C=z["C"], d=z["d"], x0=z["x"].copy(), lb=lb, ub=ub, t=1), z["x"], z["x2"]
+    if tag == "ph1":
+        fm = O.Phase1Barrier(C=z["C"], d=z["d"], x0=z["xi"].copy(), lb=lb, ub=ub, t=1)
+        xt = np.append(z["xi"], fm.s)
+        return fm, xt, xt + 0.01
+    A = [z[f"socp_A_{i}"] for i in range(int(z["socp_A_count"]))]
+    A[-1] = np.diag(A[-1]).copy()
+    b = [z[f"socp_b_{i}"] for i in range(int(z["socp_b_count"]))]
+    c = [z[f"socp_c_{i}"] for i in range(int(z["socp_c_count"]))]
+    d = list(z["socp_d"])
+    if tag == "socp":
+        fm = O.SOCPBarrier(P=z["P"], q=z["q"], A=A, b=b, c=c, d=d, lb=np.array(-5.), ub=np.array(5.),
+                           x0=z["socp_x0"].copy(), t=1)
+        return fm, z["socp_x0"], z["socp_x0"] + 0.01
+    fm = O.SOCPPhase1Barrier(A=A, b=b, c=c, d=d, x0=z["socp_xi"].copy(), lb=np.array(-5.), ub=np.array(5.), t=1)
+    xt = np.append(z["socp_xi"], fm.s)
+    return fm, xt, xt + 0.01
+
+
+@pytest.mark.parametrize("tag", ["lp", "qp", "ph1", "socp", "sph1"])
+def test_function_values(tag):
+    z = load("fm_kats")
+    fm, xv, xs = _fm_from_kats(z, tag)
+    t = float(z["t"])
+    fm.update_x(xv.copy()); fm.update_t(t)
+    assert rel(fm.slacks, z[tag + "_slacks"]) <= 1e-14
+    assert rel(fm.newton_objective(), z[tag + "_nobj"]) <= 1e-13
+    assert rel(fm.gradient(), z[tag + "_grad"]) <= 1e-13
+    assert rel(fm.hessian(), z[tag + "_hess"]) <= 1e-13
+    fm.update_x(xs.copy(), update_slacks=False)
+    assert rel(fm.newton_objective(), z[tag + "_stale_nobj"]) <= 1e-13
+    assert rel(fm.gradient(), z[tag + "_stale_grad"]) <= 1e-13
+
+
+def test_lp_diag_hessian():
+    z = load("fm_kats")
+    fm = O.LPBarrier(c=z["c"], x0=z["x"].copy(), lb=z["lb"], ub=z["ub"], t=1, try_diag=True)
+    fm.update_x(z["x"].copy()); fm.update_t(float(z["t"]))
+    assert rel(fm.gradient(), z["lpdiag_grad"]) <= 1e-14
+    assert rel(fm.hessian(), z["lpdiag_hess"]) <= 1e-14
+    assert rel(fm.inv_hessian(), z["lpdiag_ihess"]) <= 1e-14
+
+
+def oracle_solver(kind, kw):
+    cls = {"LP": O.LPSolver, "QP": O.QPSolver, "SOCP": O.SOCPSolver}[kind]
+    return cls(**kw)
+
+
+@pytest.mark.parametrize("name", sorted(SOLVE_CASES))
+def test_full_solve_matches_reference(name):
+    z = load(name)
+    kw = solver_kwargs(z)
+    kw["x0"] = z["x_init"].copy()
+    s = oracle_solver(SOLVE_CASES[name], kw)
+    val = s.solve()
+    steps = [tr["step"] for tr in (s.phase1.ns.trace if s.phase1_iters else [])] + [tr["step"] for tr in s.ns.trace]
+    assert list(s.inner_iters) == list(z["inner_iters"])
+    assert list(s.phase1_iters) == list(z["phase1_inner_iters"])
+    assert len(steps) == len(z["trace_step"])
+    np.testing.assert_allclose(steps, z["trace_step"], rtol=1e-9, atol=0)
+    assert rel(val, z["value"]) <= 1e-9
+    assert rel(s.xstar, z["xstar"]) <= 1e-9
+    assert s.ns.use_backup == bool(z["use_backup"])
+
+
+def test_group_lasso_fstar():
+    """demo.ipynb cell 31: value + Y'Y/(2N) == FSTAR (the notebook shows 8.4e-8 agreement)."""
+    z = load("socp_group_lasso")
+    kw = solver_kwargs(z)
+    kw["x0"] = z["x_init"].copy()
+    s = O.SOCPSolver(**kw)
+    v = s.solve()
+    assert abs(v + float(z["yty_over_2n"]) - float(z["fstar"])) < 1e-6
