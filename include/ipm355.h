@@ -1,0 +1,188 @@
+/*
+ * ipm355.h -- C ABI of the MI355X (gfx950) interior-point Newton hot path.
+ *
+ * Drop-in boundary for the reference's Newton inner loop
+ * (fdeguire03/InteriorPoint-GPU).  The reference is pure Python with no FFI;
+ * its seam between the problem facades (LPSolver/QPSolver/SOCPSolver) and the
+ * numerics is the "oracle protocol" of FunctionManager.py:94-195 and the
+ * Newton protocol of NewtonSolver.py:80 / NewtonSolverInfeasibleStart.py:72.
+ * Each entry point below names the reference interface it replaces.
+ * The Python binding (ctypes) lives in interiorpoint-gpu_amd/ipm355/_lib.py;
+ * INTEGRATION.md shows the stub a reference maintainer would add.
+ *
+ * Conventions
+ *   - fp64 everywhere.  Dense inputs are row-major (C order) with explicit
+ *     leading dimensions, exactly as NumPy hands them over.
+ *   - Every pointer argument marked [dev] is a device pointer (in practice a
+ *     torch tensor's data_ptr()); the library never allocates device memory on
+ *     the hot path: the caller provides a workspace of ipm_workspace_bytes().
+ *   - All work is enqueued on the handle's stream.  Entry points that return
+ *     host scalars synchronise that stream once.
+ *   - Return value: IPM_OK or an error code; ipm_last_error() has the text.
+ */
+#ifndef IPM355_H
+#define IPM355_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPM_OK 0
+#define IPM_NOT_POSITIVE_DEFINITE 1 /* LAPACK potrf info > 0 (drives Q9 fallback) */
+#define IPM_INVALID_ARG 2
+#define IPM_HIP_ERROR 3
+#define IPM_NOT_SUPPORTED 4
+
+/* problem kinds (LPSolver.py / QPSolver.py / SOCPSolver.py) */
+#define IPM_KIND_LP 0
+#define IPM_KIND_QP 1
+#define IPM_KIND_SOCP 2
+
+/* linear-solve strategies (dispatch tables LPSolver.py:371-469, QPSolver.py:385-455) */
+#define IPM_SOLVE_CHOLESKY 0 /* dense Cholesky; first failure -> permanent fallback (Q9) */
+#define IPM_SOLVE_DIAGONAL 1 /* H diagonal (LP, C is None, try_diag) */
+#define IPM_SOLVE_LU 2       /* np_solve: LU with partial pivoting */
+
+typedef struct ipm_handle ipm_handle;
+typedef struct ipm_problem ipm_problem;
+
+/*
+ * Problem description.  Mirrors the data the reference's FunctionManager*
+ * constructors receive (FunctionManager.py:13-90, 359-425, 619-680, 834-931,
+ * 1165-1256).  Absent items are NULL.  Scalar bounds are expanded to n-vectors
+ * by the caller.
+ */
+typedef struct ipm_problem_desc {
+  int32_t kind;          /* IPM_KIND_*                                           */
+  int32_t phase1;        /* 1: the phase-1 barrier (FunctionManagerPhase1 /      */
+                         /*    FunctionManagerSOCPPhase1); variables (x, s)      */
+  int32_t solve_method;  /* IPM_SOLVE_*                                          */
+  int32_t reserved0;
+  int64_t n;             /* number of x variables (without the phase-1 s)        */
+  /* objective */
+  const double* c;       /* [dev] n      LP cost (FunctionManager.py:76-90)       */
+  const double* P;       /* [dev] n x n  QP/SOCP quadratic term, row-major        */
+  int64_t ldp;
+  const double* q;       /* [dev] n      QP/SOCP linear term                      */
+  /* linear inequalities C x <= d (LP, QP, LP phase 1) */
+  int64_t m;
+  const double* C;       /* [dev] m x n  row-major                                */
+  int64_t ldc;
+  const double* d;       /* [dev] m                                               */
+  /* box bounds */
+  const double* lb;      /* [dev] n                                               */
+  const double* ub;      /* [dev] n                                               */
+  /* equality constraints A x = b -> infeasible-start Newton
+     (NewtonSolverInfeasibleStart.py; SOCPSolver passes F, g here)               */
+  int64_t p;
+  const double* A;       /* [dev] p x n  row-major                                */
+  int64_t lda;
+  const double* AT;      /* [dev] n x p  row-major copy of A^T (static, once)     */
+  const double* b;       /* [dev] p                                               */
+  /* second-order cones (FunctionManagerSOCP): ||A_i x + b_i|| <= c_i.x + d_i    */
+  int64_t K;             /* number of cones                                       */
+  int64_t R;             /* total rows of the dense cones                         */
+  double* X;             /* [dev] (R + 2K) x n row-major, ldx: rows [0,R) stacked */
+                         /*   dense A_i, rows [R,R+K) the c_i, rows [R+K,R+2K)    */
+                         /*   scratch for the per-cone gradient rows g_i          */
+  int64_t ldx;
+  const int64_t* cone_row_off; /* [dev] K+1: rows of cone i are [off[i],off[i+1]); */
+                               /*   a diagonal cone has off[i]==off[i+1]           */
+  const int64_t* cone_row_off_host; /* host copy of the above                     */
+  const double* cone_b;  /* [dev] R: b_i stacked for the dense rows (NULL: no b)   */
+  const double* cone_d;  /* [dev] K: d_i (NULL: no d)                              */
+  int32_t has_cone_c;    /* 0: no c_i (rhs_i = d_i)                                */
+  int32_t reserved1;
+  int64_t Kd;            /* number of diagonal cones (A_i = diag(a_i), SOCPSolver.py:285-292) */
+  const double* Ad;      /* [dev] Kd x n  a_i                                       */
+  const double* bd;      /* [dev] Kd x n  b_i (NULL: no b)                          */
+  const int64_t* dcone_id; /* [dev] Kd: cone index of each diagonal cone            */
+  const int64_t* dcone_id_host;
+} ipm_problem_desc;
+
+/* Newton options: NewtonSolver.__init__ (NewtonSolver.py:16-78) */
+typedef struct ipm_newton_opts {
+  int32_t max_iters;
+  int32_t update_slacks_every;   /* Q2 */
+  int32_t phase1_flag;           /* early exit x[-1] < -phase1_tol (NewtonSolver.py:105-107) */
+  int32_t use_psd_condition;     /* +1e-9 on diag before Cholesky (NewtonSolver.py:269-275) */
+  double eps;                    /* inner epsilon */
+  double alpha, beta;            /* backtracking parameters */
+  double phase1_tol;
+} ipm_newton_opts;
+
+/* Result of one centering step: the tuple NewtonSolver.solve returns */
+typedef struct ipm_newton_result {
+  int32_t iters;        /* Newton iterations taken                               */
+  int32_t success;      /* success flag                                          */
+  int32_t stat_valid;   /* 0: the reference would return None                    */
+  int32_t use_backup;   /* Cholesky fallback engaged (persists, Q9)              */
+  double stat;          /* nd = -g.dx/2 (feasible) or trial residual (infeasible)*/
+  double last_step;     /* last accepted step size                               */
+  int64_t backtracks;   /* total trial points examined                           */
+} ipm_newton_result;
+
+/* ---- handle --------------------------------------------------------------- */
+/* one handle per (process, device, stream); stream = hipStream_t or NULL */
+int ipm_create(int device, void* stream, ipm_handle** out);
+int ipm_destroy(ipm_handle* h);
+const char* ipm_last_error(ipm_handle* h);
+int ipm_version(void);
+
+/* ---- level 2: the Newton inner loop (the hot path) ------------------------- */
+/* bytes of device workspace the problem needs */
+int64_t ipm_workspace_bytes(const ipm_problem_desc* desc);
+int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, void* workspace /*[dev]*/,
+                       int64_t workspace_bytes, ipm_problem** out);
+int ipm_problem_destroy(ipm_problem* pr);
+/* NewtonSolver.solve / NewtonSolverInfeasibleStart.solve: x [dev] (N = n(+1)) is
+   updated in place (Q8); v [dev] (p) likewise; t is the barrier parameter. */
+int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v, const ipm_newton_opts* opts,
+                     ipm_newton_result* res);
+/* persistent Cholesky-failure flag (Q9) */
+int ipm_get_use_backup(ipm_problem* pr);
+int ipm_set_use_backup(ipm_problem* pr, int flag);
+
+/* ---- level 1: the oracle protocol (FunctionManager.py:94-195) ---------------- */
+/* update_x(x, update_slacks): the evaluation point becomes x [dev]; slacks are
+   recomputed only if update_slacks (Q2) */
+int ipm_fm_update_x(ipm_problem* pr, const double* x, int update_slacks);
+/* slacks [dev out] (FunctionManager.slacks) */
+int ipm_fm_slacks(ipm_problem* pr, double* out);
+int64_t ipm_fm_num_slacks(ipm_problem* pr);
+/* objective(): f(x) at the evaluation point (host scalar) */
+int ipm_fm_objective(ipm_problem* pr, double* out);
+/* newton_objective(): t f(x) - sum log(s + eps) with the CURRENT (maybe stale) slacks */
+int ipm_fm_newton_objective(ipm_problem* pr, double t, double* out);
+/* gradient() [dev out, N] */
+int ipm_fm_gradient(ipm_problem* pr, double t, double* g);
+/* hessian() [dev out]: dense N x N row-major full matrix (both triangles), or for
+   IPM_SOLVE_DIAGONAL the diagonal vector (N) */
+int ipm_fm_hessian(ipm_problem* pr, double t, double* H, int64_t ldh);
+
+/* ---- level 0: dense fp64 kernels (exposed for tests and benches) -------------- */
+/* y = alpha * op(M) x + beta * y ; M row-major rows x cols */
+int ipm_gemv(ipm_handle* h, int trans, int64_t rows, int64_t cols, double alpha, const double* M,
+             int64_t ldm, const double* x, double beta, double* y);
+/* H(lower, column-major ldh) = alpha * X^T diag(w) X + beta * H ; X row-major k x n.
+   w may be NULL (all ones).  The SYRK of FunctionManager.py:301-306 / 801-805. */
+int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, int64_t ldx, const double* w,
+             double alpha, double beta, double* H, int64_t ldh);
+/* in-place Cholesky of the lower triangle of H (column-major, ldh); *info as LAPACK
+   potrf (0 ok, j>0: leading minor j not positive definite).  work: [dev] >= 64 bytes */
+int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info);
+/* solve L L^T X = B in place; L lower column-major (ldl); B row-major n x nrhs (ldb) */
+int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
+              int64_t ldb);
+/* HIP-event timing of the KKT assembly and of the Cholesky factorisation inside
+   ipm_newton_solve (enable/reset with ipm_set_timing; adds no synchronisation):
+   averages (ms) over the Newton iterations since the reset, and their count */
+int ipm_set_timing(ipm_handle* h, int on);
+int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPM355_H */

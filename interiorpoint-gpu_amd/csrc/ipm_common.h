@@ -1,0 +1,82 @@
+// Shared device helpers and launch-wrapper declarations for the ipm355 kernels.
+// gfx950 only: wave64, fp64 MFMA (v_mfma_f64_16x16x4_f64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ipm {
+
+constexpr int WAVE = 64;
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// block-wide sum (blockDim.x multiple of 64, <= 1024); result valid in all threads
+__device__ __forceinline__ double block_sum(double v, double* red /* >= 16 doubles LDS */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int i = 0; i < nw; ++i) r += red[i];   // fixed order: deterministic
+  return r;
+}
+
+// ---------------------------------------------------------------- launch wrappers
+// dense kernels (ipm_blas.hip); all pointers are device pointers, fp64
+// y[i] = alpha * sum_j M[i*ldm + j] x[j] + beta * y[i]        (rows x cols, row-major)
+void gemv_n(hipStream_t s, int64_t rows, int64_t cols, double alpha, const double* M, int64_t ldm,
+            const double* x, double beta, double* y);
+// y[j] = alpha * sum_i w[i] M[i*ldm + j] x[i] + beta * y[j]   (w may be null)
+void gemv_t(hipStream_t s, int64_t rows, int64_t cols, double alpha, const double* M, int64_t ldm,
+            const double* x, const double* w, double beta, double* y, double* partial_ws,
+            int64_t partial_ws_elems);
+int64_t gemv_t_ws_elems(int64_t rows, int64_t cols);
+
+// lower triangle (column-major, ldh) of  H = alpha * X^T diag(w) Y + beta * H + tP * P + diag(dvec)
+// X, Y row-major k x n (ld ldx, ldy).  w, P, dvec may be null.  Y may equal X.
+struct SyrkEpi {
+  const double* P = nullptr;   // row-major symmetric, ldp
+  int64_t ldp = 0;
+  double tP = 0.0;
+  const double* dvec = nullptr;
+};
+void syrk_lower(hipStream_t s, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
+                const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
+                const SyrkEpi& epi);
+// C(m x n, column-major ldc) -= A(m x k, col-major lda) * B(n x k, col-major ldb)^T
+//   (the GEMM of the Cholesky panel / trailing update, general rectangle)
+void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A, int64_t lda,
+                 const double* B, int64_t ldb, double* C, int64_t ldc);
+
+// Cholesky (column-major lower, in place). info_dev: device int (0 or first failing column, 1-based)
+void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev);
+// L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs
+void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
+                 int64_t ldb, double* W);
+// forward L Y = B / backward L^T Y = B: B is consumed, the solution goes to Y (same ld)
+void trsm_lower_fwd(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
+                    int64_t ldb, double* Y);
+void trsm_lower_bwd(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
+                    int64_t ldb, double* Y);
+// LU with partial pivoting (row-major in/out copy in column-major work), solve; used as the
+// Cholesky fallback (NewtonSolver.py:334-341, NewtonSolverInfeasibleStart.py:513-538)
+void getrf(hipStream_t s, int64_t n, double* A, int64_t lda, int64_t* piv, int* info_dev);
+void getrs(hipStream_t s, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
+           double* B, int64_t ldb);
+
+// small helpers
+void fill(hipStream_t s, double* p, int64_t n, double v);
+void copy(hipStream_t s, double* dst, const double* src, int64_t n);
+// dst(col-major lower, ldd) full symmetric expansion into row-major full out (ldo)
+void sym_lower_to_full(hipStream_t s, int64_t n, const double* L, int64_t ldl, double* out, int64_t ldo);
+void transpose(hipStream_t s, int64_t rows, int64_t cols, const double* in, int64_t ldi, double* out,
+               int64_t ldo);
+
+}  // namespace ipm

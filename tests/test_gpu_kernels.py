@@ -1,0 +1,78 @@
+"""-m gpu: the dense fp64 kernels against a NumPy fp64 reference of the same op.
+
+Tolerances: fp64 sums of k products in a different order -> |err| <= 64 eps * sum|a*b|.
+"""
+import numpy as np
+import pytest
+
+from gpu_util import colmajor_lower, dev, host, potrf, potrs, syrk
+
+pytestmark = pytest.mark.gpu
+EPS = np.finfo(np.float64).eps
+
+
+@pytest.mark.parametrize("k,n", [(4, 16), (1, 1), (16, 128), (37, 130), (300, 257), (512, 1024), (0, 5)])
+def test_syrk_weighted_matches_numpy(k, n):
+    rng = np.random.default_rng(k * 1000 + n)
+    X = rng.uniform(-2, 2, (k, n))
+    w = rng.uniform(0.1, 3, k)
+    H = syrk(X, w, n)
+    ref = X.T @ (w[:, None] * X)
+    bound = 64 * EPS * (np.abs(X).T @ (w[:, None] * np.abs(X))) + 1e-300
+    got = colmajor_lower(H, n)
+    assert np.all(np.abs(np.tril(got - ref)) <= np.tril(bound) + 1e-14 * (k == 0))
+
+
+def test_syrk_fragment_layout_asymmetric():
+    """A = I-style check with an asymmetric operand (cdna_hip_programming.md §3 warning)."""
+    n, k = 64, 64
+    X = np.zeros((k, n))
+    for i in range(k):
+        X[i, i] = 1.0
+    X[3, 17] = 5.0   # makes H[3][17] = H[17][3] = 5 and H[17][17] = 26
+    H = colmajor_lower(syrk(X, None, n), n)
+    ref = np.tril(X.T @ X)
+    np.testing.assert_array_equal(H, ref)
+
+
+def test_syrk_odd_ld_and_beta():
+    rng = np.random.default_rng(3)
+    n, k, ldh = 75, 33, 79
+    X = rng.normal(size=(k, n))
+    H0 = rng.normal(size=(n, ldh))
+    H = syrk(X, None, n, ldh=ldh, beta=1.0, H0=H0, alpha=-1.0)
+    M0 = H0.T[:n, :n]
+    ref = np.tril(M0 - X.T @ X)
+    got = colmajor_lower(H, n)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * (1 + np.abs(X).max() ** 2 * k))
+
+
+@pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 513, 1030])
+def test_potrf_potrs_match_numpy(n):
+    rng = np.random.default_rng(n)
+    M = rng.normal(size=(n + 5, n))
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A.T.copy())  # column-major A == row-major A^T (symmetric anyway)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 0 and info == 0
+    L = colmajor_lower(Hm, n)
+    Lr = np.linalg.cholesky(A)
+    np.testing.assert_allclose(L, Lr, rtol=1e-10, atol=1e-10 * np.abs(Lr).max())
+    b = rng.normal(size=(n, 3))
+    x = potrs(Hm, n, n, b.copy())
+    np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-9, atol=1e-12)
+
+
+def test_potrf_reports_lapack_info():
+    n = 150
+    rng = np.random.default_rng(0)
+    M = rng.normal(size=(n, n))
+    A = M @ M.T + np.eye(n)
+    A[97, 97] = -1e6        # leading minor 98 is not PD
+    Hm = dev(A)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 1
+    import scipy.linalg
+    with pytest.raises(np.linalg.LinAlgError) as e:
+        scipy.linalg.cho_factor(A)
+    assert f"{info}-th leading minor" in str(e.value)

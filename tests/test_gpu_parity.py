@@ -1,0 +1,107 @@
+"""-m gpu: the HIP path against the reference's golden vectors (and the oracle).
+
+Tolerances (stated per the north star): x* within 1e-6 relative error of the
+reference NumPy solve; per-function oracle values within 1e-10 relative (fp64
+sums in a different order); trajectories (inner-iteration counts) must match.
+"""
+import numpy as np
+import pytest
+
+from golden_io import SOLVE_CASES, load, solver_kwargs
+
+pytestmark = pytest.mark.gpu
+
+XSTAR_RTOL = 1e-6
+FN_RTOL = 1e-10
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _device_fm(z, tag):
+    import ipm355
+    lb, ub = z["lb"], z["ub"]
+    if tag == "lp":
+        return ipm355.FunctionManagerLP(c=z["c"], C=z["C"], d=z["d"], x0=z["x"].copy(), lower_bound=lb,
+                                        upper_bound=ub, t=1), z["x"], z["x2"]
+    if tag == "qp":
+        return ipm355.FunctionManagerQP(P=z["P"], q=z["q"], C=z["C"], d=z["d"], x0=z["x"].copy(),
+                                        lower_bound=lb, upper_bound=ub, t=1), z["x"], z["x2"]
+    if tag == "ph1":
+        fm = ipm355.FunctionManagerPhase1(C=z["C"], d=z["d"], x0=z["xi"].copy(), lower_bound=lb, upper_bound=ub, t=1)
+        assert abs(fm.s - float(z["ph1_s0"])) <= 1e-12 * abs(float(z["ph1_s0"]))
+        xt = np.append(z["xi"], float(z["ph1_s0"]))
+        return fm, xt, xt + 0.01
+    A = [z[f"socp_A_{i}"] for i in range(int(z["socp_A_count"]))]
+    A[-1] = np.diag(A[-1]).copy()
+    b = [z[f"socp_b_{i}"] for i in range(int(z["socp_b_count"]))]
+    c = [z[f"socp_c_{i}"] for i in range(int(z["socp_c_count"]))]
+    d = [float(v) for v in z["socp_d"]]
+    if tag == "socp":
+        fm = ipm355.FunctionManagerSOCP(P=z["P"], q=z["q"], A=A, b=b, c=c, d=d, lower_bound=-5.0, upper_bound=5.0,
+                                        x0=z["socp_x0"].copy(), t=1)
+        return fm, z["socp_x0"], z["socp_x0"] + 0.01
+    fm = ipm355.FunctionManagerSOCPPhase1(A=A, b=b, c=c, d=d, x0=z["socp_xi"].copy(), lower_bound=-5.0,
+                                          upper_bound=5.0, t=1)
+    assert abs(fm.s - float(z["sph1_s0"])) <= 1e-12 * abs(float(z["sph1_s0"]))
+    xt = np.append(z["socp_xi"], float(z["sph1_s0"]))
+    return fm, xt, xt + 0.01
+
+
+@pytest.mark.parametrize("tag", ["lp", "qp", "ph1", "socp", "sph1"])
+def test_oracle_protocol_values(tag):
+    z = load("fm_kats")
+    fm, xv, xs = _device_fm(z, tag)
+    t = float(z["t"])
+    fm.update_x(xv.copy())
+    fm.update_t(t)
+    assert rel(fm.slacks, z[tag + "_slacks"]) <= FN_RTOL
+    assert rel(fm.newton_objective(), z[tag + "_nobj"]) <= FN_RTOL
+    assert rel(fm.gradient(), z[tag + "_grad"]) <= FN_RTOL
+    assert rel(fm.hessian(), z[tag + "_hess"]) <= FN_RTOL
+    fm.update_x(xs.copy(), update_slacks=False)          # Q2: stale slacks
+    assert rel(fm.newton_objective(), z[tag + "_stale_nobj"]) <= FN_RTOL
+    assert rel(fm.gradient(), z[tag + "_stale_grad"]) <= FN_RTOL
+
+
+def test_lp_diagonal_hessian():
+    import ipm355
+    z = load("fm_kats")
+    fm = ipm355.FunctionManagerLP(c=z["c"], x0=z["x"].copy(), lower_bound=z["lb"], upper_bound=z["ub"], t=1,
+                                  try_diag=True)
+    fm.update_x(z["x"].copy())
+    fm.update_t(float(z["t"]))
+    assert rel(fm.gradient(), z["lpdiag_grad"]) <= FN_RTOL
+    assert rel(fm.hessian(), z["lpdiag_hess"]) <= FN_RTOL
+    assert rel(fm.inv_hessian(), z["lpdiag_ihess"]) <= FN_RTOL
+
+
+def _run(name):
+    import ipm355
+    z = load(name)
+    kw = solver_kwargs(z)
+    kw["x0"] = z["x_init"].copy()
+    kw["check_cvxpy"] = False
+    kw["suppress_print"] = True
+    cls = {"LP": ipm355.LPSolver, "QP": ipm355.QPSolver, "SOCP": ipm355.SOCPSolver}[SOLVE_CASES[name]]
+    s = cls(**kw)
+    v = s.solve()
+    return z, s, v
+
+
+@pytest.mark.parametrize("name", sorted(SOLVE_CASES))
+def test_full_solve_matches_reference(name):
+    z, s, v = _run(name)
+    assert rel(s.xstar, z["xstar"]) <= XSTAR_RTOL, (rel(s.xstar, z["xstar"]), list(s.inner_iters),
+                                                    list(z["inner_iters"]))
+    assert abs(v - float(z["value"])) <= 1e-7 * max(1.0, abs(float(z["value"])))
+    assert list(s.inner_iters) == list(z["inner_iters"])
+
+
+def test_group_lasso_fstar_known_answer():
+    """demo.ipynb cell 31: exercises the Cholesky-failure fallback in SOCP phase 1."""
+    z, s, v = _run("socp_group_lasso")
+    assert abs(v + float(z["yty_over_2n"]) - float(z["fstar"])) < 1e-6
+    assert s.phase1_solver.phase1_ns.use_backup
