@@ -111,6 +111,9 @@ typedef struct ipm_newton_opts {
   double eps;                    /* inner epsilon */
   double alpha, beta;            /* backtracking parameters */
   double phase1_tol;
+  double* trace;                 /* optional HOST buffer: per-iteration (step, stat) pairs  */
+  int32_t trace_cap;             /* capacity in iterations (0: no trace)                   */
+  int32_t reserved;
 } ipm_newton_opts;
 
 /* Result of one centering step: the tuple NewtonSolver.solve returns */
@@ -125,7 +128,7 @@ typedef struct ipm_newton_result {
 } ipm_newton_result;
 
 /* ---- handle --------------------------------------------------------------- */
-/* one handle per (process, device, stream); stream = hipStream_t or NULL */
+/* one handle per (process, device, stream); stream = hipStream_t, NULL = legacy default stream */
 int ipm_create(int device, void* stream, ipm_handle** out);
 int ipm_destroy(ipm_handle* h);
 const char* ipm_last_error(ipm_handle* h);

@@ -415,12 +415,9 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   h->device = device;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete h; return IPM_HIP_ERROR; }
-  if (stream) {
-    h->stream = (hipStream_t)stream;
-  } else {
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
-    h->own_stream = true;
-  }
+  // NULL = the legacy default stream (what torch's default stream is), so work is ordered
+  // with the caller's tensor initialisation and reads without extra events.
+  h->stream = (hipStream_t)stream;
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   for (auto& ev : h->ev) hipEventCreate(&ev);
@@ -1033,6 +1030,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       }
       axpy(st, pr->N, step, pr->dx, x);
       res->last_step = step;
+      if (o->trace && it < o->trace_cap) { o->trace[2 * it] = step; o->trace[2 * it + 1] = -rb.sc[SC_GDX] / 2; }
       if (pr->ph1 && o->phase1_flag) {
         const double xn = rb.sc[SC_XN] + step * rb.sc[SC_DXN];
         if (xn < -o->phase1_tol) return finish(it + 1, true, false, 0.0);
@@ -1152,6 +1150,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       axpy(st, pr->N, step, pr->dx, x);
       axpy(st, pr->p, step, pr->dv, v);
       res->last_step = step;
+      if (o->trace && it < o->trace_cap) { o->trace[2 * it] = step; o->trace[2 * it + 1] = have_rn ? rn : NAN; }
       stat = rn;
       stat_valid = have_rn;
       if (step < STEP_FLOOR) return finish(it + 1, false, have_rn, rn);

@@ -51,7 +51,7 @@ class ProblemDesc(C.Structure):
 class NewtonOpts(C.Structure):
     _fields_ = [("max_iters", I32), ("update_slacks_every", I32), ("phase1_flag", I32),
                 ("use_psd_condition", I32), ("eps", F64), ("alpha", F64), ("beta", F64),
-                ("phase1_tol", F64)]
+                ("phase1_tol", F64), ("trace", C.POINTER(F64)), ("trace_cap", I32), ("reserved", I32)]
 
 
 class NewtonResult(C.Structure):

@@ -6,7 +6,7 @@ everything the Newton loop touches afterwards stays on the device.
 """
 from __future__ import annotations
 
-import ctypes as C
+import ctypes as ct
 
 import numpy as np
 
@@ -109,22 +109,22 @@ class DeviceProblem:
         if cones is not None:
             desc.K, desc.R, desc.X, desc.ldx = cones.K, cones.R, dp(cones.X), n
             desc.cone_row_off = dp(cones.off)
-            desc.cone_row_off_host = cones.off_host.ctypes.data_as(C.c_void_p)
+            desc.cone_row_off_host = cones.off_host.ctypes.data_as(ct.c_void_p)
             desc.cone_b, desc.cone_d = dp(cones.cb), dp(cones.cd)
             desc.has_cone_c = 1 if cones.has_c else 0
             desc.Kd = cones.Kd
             desc.Ad, desc.bd = dp(cones.Ad), dp(cones.bd)
             desc.dcone_id = dp(cones.dids)
-            desc.dcone_id_host = cones.dids_host.ctypes.data_as(C.c_void_p)
+            desc.dcone_id_host = cones.dids_host.ctypes.data_as(ct.c_void_p)
         self.desc = desc
         lib = self.handle.lib
-        nbytes = lib.ipm_workspace_bytes(C.byref(desc))
+        nbytes = lib.ipm_workspace_bytes(ct.byref(desc))
         if nbytes <= 0:
             raise L.IPMBackendError("ipm_workspace_bytes failed")
         self.ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        ptr = C.c_void_p()
-        self.handle.check(lib.ipm_problem_create(self.handle.ptr, C.byref(desc), L.dptr(self.ws),
-                                                 int(nbytes), C.byref(ptr)), self.handle.ptr)
+        ptr = ct.c_void_p()
+        self.handle.check(lib.ipm_problem_create(self.handle.ptr, ct.byref(desc), L.dptr(self.ws),
+                                                 int(nbytes), ct.byref(ptr)), self.handle.ptr)
         self.ptr = ptr
         self.num_slacks = int(lib.ipm_fm_num_slacks(ptr))
 
@@ -149,9 +149,15 @@ class DeviceProblem:
         o = L.NewtonOpts(int(max_iters), int(update_slacks_every), 1 if phase1_flag else 0,
                          1 if use_psd_condition else 0, float(eps), float(alpha), float(beta),
                          float(phase1_tol))
+        cap = int(max_iters)
+        buf = (ct.c_double * (2 * max(cap, 1)))()
+        o.trace = ct.cast(buf, ct.POINTER(ct.c_double))
+        o.trace_cap = cap
         r = L.NewtonResult()
-        self.check(self.handle.lib.ipm_newton_solve(self.ptr, L.dptr(x), float(t), L.dptr(v), C.byref(o),
-                                                    C.byref(r)))
+        self.check(self.handle.lib.ipm_newton_solve(self.ptr, L.dptr(x), float(t), L.dptr(v), ct.byref(o),
+                                                    ct.byref(r)))
+        k = min(int(r.iters), cap)
+        self.last_trace = [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
         return r
 
     @property
@@ -174,13 +180,13 @@ class DeviceProblem:
         return out
 
     def fm_objective(self):
-        v = C.c_double()
-        self.check(self.handle.lib.ipm_fm_objective(self.ptr, C.byref(v)))
+        v = ct.c_double()
+        self.check(self.handle.lib.ipm_fm_objective(self.ptr, ct.byref(v)))
         return v.value
 
     def fm_newton_objective(self, t):
-        v = C.c_double()
-        self.check(self.handle.lib.ipm_fm_newton_objective(self.ptr, float(t), C.byref(v)))
+        v = ct.c_double()
+        self.check(self.handle.lib.ipm_fm_newton_objective(self.ptr, float(t), ct.byref(v)))
         return v.value
 
     def fm_gradient(self, t):

@@ -47,6 +47,7 @@ class NewtonSolver:
         if self.method == "lu" and self.fm is not None:
             self.fm.prob.use_backup = True       # np.linalg.solve / lstsq / inv from the start
         self.last_result = None
+        self.trace = []          # per-iteration (step, nd | residual) like the oracle's trace
 
     @property
     def use_backup(self):
@@ -68,6 +69,7 @@ class NewtonSolver:
                               phase1_flag=self.phase1_flag, phase1_tol=self.phase1_tol,
                               use_psd_condition=self.use_psd_condition)
         self.last_result = r
+        self.trace.extend(prob.last_trace)
         self.fm._x.copy_(xd.reshape(-1)) if xd.numel() == prob.N else None
         if copied:
             np.copyto(x, xd.cpu().numpy())

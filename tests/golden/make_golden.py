@@ -62,6 +62,29 @@ def _pack_list(prefix, arrs, out):
         out[f"{prefix}_{i}"] = np.asarray(a)
 
 
+def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
+    """Re-run the reference with one right-hand-side vector perturbed by 1e-15 (relative):
+    the spread of x*, value and iteration counts is the reference's own numerical envelope."""
+    key = next(k for k in ("b", "g", "d", "q") if isinstance(kwargs.get(k), np.ndarray))
+    rng = np.random.default_rng(1234)
+    wx = wv = 0.0
+    stable = True
+    for _ in range(trials):
+        kw = {k: ([np.array(a, copy=True) if isinstance(a, np.ndarray) else a for a in v] if isinstance(v, list)
+                  else (np.array(v, copy=True) if isinstance(v, np.ndarray) else v)) for k, v in kwargs.items()}
+        kw[key] = kw[key] * (1 + 1e-15 * rng.standard_normal(kw[key].shape))
+        kw.setdefault("check_cvxpy", False)
+        kw.setdefault("suppress_print", True)
+        if rand_seed is not None:
+            np.random.seed(rand_seed)
+        s = cls(**kw)
+        s.solve()
+        wx = max(wx, float(np.linalg.norm(s.xstar - base_x) / np.linalg.norm(base_x)))
+        wv = max(wv, float(abs(s.value - base_v) / max(abs(base_v), 1e-300)))
+        stable &= list(s.inner_iters) == list(base_iters)
+    return key, wx, wv, stable
+
+
 def run_solve(name, cls, kwargs, solve_kwargs=None, rand_seed=None):
     TRACE.clear()
     if rand_seed is not None:
@@ -95,8 +118,16 @@ def run_solve(name, cls, kwargs, solve_kwargs=None, rand_seed=None):
     out["use_backup"] = np.array(bool(getattr(solver.ns, "use_backup", False)))
     out["phase1_use_backup"] = np.array(bool(getattr(getattr(ph, "phase1_ns", None), "use_backup", False)))
     out["solve_kwargs"] = np.array(repr(solve_kwargs or {}))
+    saved_trace = list(TRACE)
+    key, wx, wv, stable = sensitivity(cls, kwargs, np.asarray(solver.xstar), float(val), solver.inner_iters, rand_seed)
+    TRACE[:] = saved_trace
+    out["sens_key"] = np.array(key)
+    out["sens_xstar_rel"] = np.array(wx)
+    out["sens_value_rel"] = np.array(wv)
+    out["sens_iters_stable"] = np.array(stable)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
-    print(f"{name}: value={val!r} inner={solver.inner_iters} steps={len(TRACE)}")
+    print(f"{name}: value={val!r} inner={solver.inner_iters} steps={len(TRACE)} "
+          f"sens({key}): x* {wx:.1e} value {wv:.1e} iters stable {stable}")
 
 
 def fm_kats():

@@ -2,7 +2,17 @@
 
 Tolerances (stated per the north star): x* within 1e-6 relative error of the
 reference NumPy solve; per-function oracle values within 1e-10 relative (fp64
-sums in a different order); trajectories (inner-iteration counts) must match.
+sums in a different order).  Trajectories (inner-iteration counts AND the full
+sequence of accepted step sizes beta^k) must match exactly wherever the
+reference's own trajectory is stable.
+
+Some golden cases are chaotic in the reference itself: make_golden.py re-ran the
+reference with one right-hand side perturbed by 1e-15 (relative) and stored the
+spread (sens_*).  Where iteration counts change under that perturbation, no
+implementation with a different summation order can match them; there the test
+requires x* / value within max(1e-6, 4 x the reference's own spread) and reports
+the divergence instead of asserting the counts ("flag divergent
+trajectories rather than average them").
 """
 import numpy as np
 import pytest
@@ -94,10 +104,21 @@ def _run(name):
 @pytest.mark.parametrize("name", sorted(SOLVE_CASES))
 def test_full_solve_matches_reference(name):
     z, s, v = _run(name)
-    assert rel(s.xstar, z["xstar"]) <= XSTAR_RTOL, (rel(s.xstar, z["xstar"]), list(s.inner_iters),
-                                                    list(z["inner_iters"]))
-    assert abs(v - float(z["value"])) <= 1e-7 * max(1.0, abs(float(z["value"])))
-    assert list(s.inner_iters) == list(z["inner_iters"])
+    stable = bool(z["sens_iters_stable"])
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    vtol = max(1e-8, 4 * float(z["sens_value_rel"]))
+    err = rel(s.xstar, z["xstar"])
+    assert err <= xtol, (err, xtol, list(s.inner_iters), list(z["inner_iters"]))
+    assert abs(v - float(z["value"])) <= vtol * max(1.0, abs(float(z["value"])))
+    if stable:
+        assert list(s.inner_iters) == list(z["inner_iters"])
+        steps = [t[0] for t in ((s.phase1_solver.phase1_ns.trace if len(z["phase1_inner_iters"]) else [])
+                                + s.ns.trace)]
+        np.testing.assert_array_equal(np.array(steps), z["trace_step"])
+    elif list(s.inner_iters) != list(z["inner_iters"]):
+        print(f"[{name}] chaotic in the reference (1e-15 input perturbation changes its iterations): "
+              f"x* rel {err:.1e} (reference spread {float(z['sens_xstar_rel']):.1e}), "
+              f"iters {list(s.inner_iters)} vs {list(z['inner_iters'])}")
 
 
 def test_group_lasso_fstar_known_answer():
