@@ -127,123 +127,137 @@ void gemv_t(hipStream_t st, int64_t rows, int64_t cols, double alpha, const doub
                      beta, y);
 }
 
-// =====================================================================================
-// SYRK / GEMM^T on fp64 MFMA (v_mfma_f64_16x16x4_f64)
-//
-//   H(i,j) = alpha * sum_k w[k] X[k][i] Y[k][j] + beta*H(i,j) + tP*P[j][i] + [i==j] dvec[i]
-//   for the lower triangle i >= j; H column-major (element (i,j) at j*ldh + i).
-//
-// 128x128 output tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA tiles),
-// K staged 16 rows at a time through LDS (register prefetch of the next K-slab).
-// f64 MFMA fragment maps (cdna_hip_programming.md §3): A: lane l holds A[l&15][l>>4];
-// B: lane l holds B[l>>4][l&15]; D: lane l holds D[(l>>4)+4r][l&15], r=0..3.
-// We put j (the output column) on the MFMA row and i (output row) on the MFMA column so that
-// 16 consecutive lanes store 16 consecutive doubles of a column-major H column.
-// =====================================================================================
-constexpr int SK_BN = 128;   // output tile
+// ---- shared fp64 MFMA tile machinery (SYRK / GEMM)
 constexpr int SK_BK = 16;    // K slab
-constexpr int SK_LDS = 144;  // padded LDS row (doubles): 288 dwords == 32 mod 64 -> no 2-way conflict
+// padded LDS row (doubles): BN + 16  -> 2*(BN+16) dwords == 32 mod 64: the two k-rows a
+// wave reads with one ds_read_b64 land in different bank halves (no 2-way conflict)
+template <int BN>
+struct Tile {
+  static constexpr int LDS = BN + 16;
+  static constexpr int TW = BN / 32;              // 16x16 MFMA tiles per wave per dim (2x2 waves)
+  static constexpr int NPT = SK_BK * BN / 256;    // doubles staged per thread per slab
+  static constexpr int TPR = BN / NPT;            // threads per slab row
+};
 
-template <bool VEC, bool SYM>
-__global__ __launch_bounds__(256, 1) void k_syrk_lower(
-    int64_t n, int64_t K, double alpha, const double* __restrict__ X, int64_t ldx,
-    const double* __restrict__ Y, int64_t ldy, const double* __restrict__ w, double beta,
-    double* __restrict__ H, int64_t ldh, const double* __restrict__ P, int64_t ldp, double tP,
-    const double* __restrict__ dvec, const int* __restrict__ info, int64_t tiles_n) {
-  if (info && *info != 0) return;
-  // lower-triangular tile index -> (bi >= bj)
-  const int64_t L = blockIdx.x;
-  int64_t bi = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= L) ++bi;
-  while (bi * (bi + 1) / 2 > L) --bi;
-  const int64_t bj = L - bi * (bi + 1) / 2;
-  const int64_t I0 = bi * SK_BN, J0 = bj * SK_BN;
-
-  __shared__ double sX[2][SK_BK * SK_LDS];  // i side (weighted)
-  __shared__ double sY[2][SK_BK * SK_LDS];  // j side
-
+// Shared MFMA main loop: acc[tj][ti] += sum_k Xw[k][I0+i] * Yv[k][J0+j]
+//   xrow(k) / yrow(k): row pointers (k-major operands), optional weight on the X side.
+template <int BN, bool VEC>
+__device__ __forceinline__ void mfma_tile(int64_t K, int64_t I0, int64_t J0, int64_t ni, int64_t nj,
+                                          const double* __restrict__ X, int64_t ldx,
+                                          const double* __restrict__ Y, int64_t ldy,
+                                          const double* __restrict__ w, double* sX, double* sY,
+                                          dbl4 (&acc)[Tile<BN>::TW][Tile<BN>::TW]) {
+  using T = Tile<BN>;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wj = wv >> 1, wi = wv & 1;
-  // staging assignment: row r = tid>>4 (0..15), 8 consecutive columns from (tid&15)*8
-  const int sr = tid >> 4, sc = (tid & 15) * 8;
-
-  dbl4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-
-  double rx[8], ry[8];
+  const int sr = tid / T::TPR, sc = (tid % T::TPR) * T::NPT;
+  double rx[T::NPT], ry[T::NPT];
   auto load_slab = [&](int64_t k0) {
     const int64_t k = k0 + sr;
     const bool kin = k < K;
     const double wk = (kin && w) ? w[k] : 1.0;
     const double* xr = X + k * ldx;
-    const double* yr = (SYM ? X : Y) + k * (SYM ? ldx : ldy);
-    if (VEC && kin && I0 + sc + 8 <= n && J0 + sc + 8 <= n) {
+    const double* yr = Y + k * ldy;
+    if (VEC && kin && I0 + sc + T::NPT <= ni && J0 + sc + T::NPT <= nj) {
       const double2* x2 = reinterpret_cast<const double2*>(xr + I0 + sc);
       const double2* y2 = reinterpret_cast<const double2*>(yr + J0 + sc);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < T::NPT / 2; ++q) {
         double2 a = x2[q], b = y2[q];
         rx[2 * q] = a.x * wk; rx[2 * q + 1] = a.y * wk;
         ry[2 * q] = b.x; ry[2 * q + 1] = b.y;
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < T::NPT; ++q) {
         const int64_t ci = I0 + sc + q, cj = J0 + sc + q;
-        rx[q] = (kin && ci < n) ? xr[ci] * wk : 0.0;
-        ry[q] = (kin && cj < n) ? yr[cj] : 0.0;
+        rx[q] = (kin && ci < ni) ? xr[ci] * wk : 0.0;
+        ry[q] = (kin && cj < nj) ? yr[cj] : 0.0;
       }
     }
   };
   auto store_slab = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      sX[buf][sr * SK_LDS + sc + q] = rx[q];
-      sY[buf][sr * SK_LDS + sc + q] = ry[q];
+    for (int q = 0; q < T::NPT; ++q) {
+      sX[buf * SK_BK * T::LDS + sr * T::LDS + sc + q] = rx[q];
+      sY[buf * SK_BK * T::LDS + sr * T::LDS + sc + q] = ry[q];
     }
   };
-
   const int64_t nslab = (K + SK_BK - 1) / SK_BK;
-  if (nslab > 0) {
-    load_slab(0);
-    store_slab(0);
-  }
+  if (nslab > 0) { load_slab(0); store_slab(0); }
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   for (int64_t s = 0; s < nslab; ++s) {
     const int buf = s & 1;
     if (s + 1 < nslab) load_slab((s + 1) * SK_BK);
+    const double* bx = sX + buf * SK_BK * T::LDS;
+    const double* by = sY + buf * SK_BK * T::LDS;
 #pragma unroll
     for (int kk = 0; kk < SK_BK / 4; ++kk) {
-      const int krow = (kk * 4 + fk) * SK_LDS;
-      double a[4], b[4];
+      const int krow = (kk * 4 + fk) * T::LDS;
+      double a[T::TW], b[T::TW];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[t] = sY[buf][krow + wj * 64 + t * 16 + fr];
-        b[t] = sX[buf][krow + wi * 64 + t * 16 + fr];
+      for (int t = 0; t < T::TW; ++t) {
+        a[t] = by[krow + wj * (BN / 2) + t * 16 + fr];
+        b[t] = bx[krow + wi * (BN / 2) + t * 16 + fr];
       }
 #pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
+      for (int tj = 0; tj < T::TW; ++tj)
 #pragma unroll
-        for (int ti = 0; ti < 4; ++ti)
+        for (int ti = 0; ti < T::TW; ++ti)
           acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tj], b[ti], acc[tj][ti], 0, 0, 0);
     }
     if (s + 1 < nslab) store_slab(buf ^ 1);
     __syncthreads();
   }
+}
 
-  // epilogue: lower triangle only
+// =====================================================================================
+// SYRK / GEMM^T on fp64 MFMA (v_mfma_f64_16x16x4_f64)
+//
+//   H(i,j) = alpha * sum_k w[k] X[k][i] Y[k][j] + beta*H(i,j) + tP*P[j][i] + [i==j] dvec[i]
+//   for the lower triangle i >= j; H column-major (element (i,j) at j*ldh + i).
+//
+// BN x BN output tile per 256-thread workgroup (2x2 waves), K staged 16 rows at a time
+// through LDS with a register prefetch of the next slab.  BN = 128 for large grids,
+// 64 when the 128-tile grid would leave CUs idle.
+// f64 MFMA fragment maps (cdna_hip_programming.md §3): A: lane l holds A[l&15][l>>4];
+// B: lane l holds B[l>>4][l&15]; D: lane l holds D[(l>>4)+4r][l&15], r=0..3.
+// j (output column) is the MFMA row and i (output row) the MFMA column, so 16
+// consecutive lanes store 16 consecutive doubles of a column-major H column.
+// =====================================================================================
+template <int BN, bool VEC, bool SYM>
+__global__ __launch_bounds__(256) void k_syrk_lower(
+    int64_t n, int64_t K, double alpha, const double* __restrict__ X, int64_t ldx,
+    const double* __restrict__ Y, int64_t ldy, const double* __restrict__ w, double beta,
+    double* __restrict__ H, int64_t ldh, const double* __restrict__ P, int64_t ldp, double tP,
+    const double* __restrict__ dvec, const int* __restrict__ info, int64_t tiles_n) {
+  using T = Tile<BN>;
+  if (info && *info != 0) return;
+  const int64_t L = blockIdx.x;
+  int64_t bi = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= L) ++bi;
+  while (bi * (bi + 1) / 2 > L) --bi;
+  const int64_t bj = L - bi * (bi + 1) / 2;
+  const int64_t I0 = bi * BN, J0 = bj * BN;
+  __shared__ double sX[2 * SK_BK * T::LDS];
+  __shared__ double sY[2 * SK_BK * T::LDS];
+  dbl4 acc[T::TW][T::TW];
 #pragma unroll
-  for (int tj = 0; tj < 4; ++tj) {
+  for (int a = 0; a < T::TW; ++a)
 #pragma unroll
-    for (int ti = 0; ti < 4; ++ti) {
-      const int64_t i = I0 + wi * 64 + ti * 16 + fr;
+    for (int b = 0; b < T::TW; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  mfma_tile<BN, VEC>(K, I0, J0, n, n, X, ldx, SYM ? X : Y, SYM ? ldx : ldy, w, sX, sY, acc);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wj = wv >> 1, wi = wv & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int tj = 0; tj < T::TW; ++tj) {
+#pragma unroll
+    for (int ti = 0; ti < T::TW; ++ti) {
+      const int64_t i = I0 + wi * (BN / 2) + ti * 16 + fr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t j = J0 + wj * 64 + tj * 16 + fk + 4 * r;
+        const int64_t j = J0 + wj * (BN / 2) + tj * 16 + fk + 4 * r;
         if (i < n && j < n && i >= j) {
           double v = alpha * acc[tj][ti][r];
           double* hp = H + j * ldh + i;
@@ -257,11 +271,11 @@ __global__ __launch_bounds__(256, 1) void k_syrk_lower(
   }
 }
 
-static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X,
-                        int64_t ldx, const double* Y, int64_t ldy, const double* w, double beta,
-                        double* H, int64_t ldh, const SyrkEpi& e, const int* info) {
-  if (n <= 0) return;
-  const int64_t T = cdiv(n, SK_BN);
+template <int BN>
+static void syrk_launch_bn(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
+                           const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
+                           const SyrkEpi& e, const int* info) {
+  const int64_t T = cdiv(n, BN);
   const int64_t nblk = T * (T + 1) / 2;
   const bool sym = (Y == nullptr) || (Y == X && ldy == ldx);
   bool vec = ((ldx & 1) == 0) && ((((uintptr_t)X) & 15) == 0);
@@ -269,13 +283,24 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
   dim3 g(nblk), b(256);
 #define SK_ARGS n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e.P, e.ldp, e.tP, e.dvec, info, T
   if (sym) {
-    if (vec) hipLaunchKernelGGL((k_syrk_lower<true, true>), g, b, 0, st, SK_ARGS);
-    else hipLaunchKernelGGL((k_syrk_lower<false, true>), g, b, 0, st, SK_ARGS);
+    if (vec) hipLaunchKernelGGL((k_syrk_lower<BN, true, true>), g, b, 0, st, SK_ARGS);
+    else hipLaunchKernelGGL((k_syrk_lower<BN, false, true>), g, b, 0, st, SK_ARGS);
   } else {
-    if (vec) hipLaunchKernelGGL((k_syrk_lower<true, false>), g, b, 0, st, SK_ARGS);
-    else hipLaunchKernelGGL((k_syrk_lower<false, false>), g, b, 0, st, SK_ARGS);
+    if (vec) hipLaunchKernelGGL((k_syrk_lower<BN, true, false>), g, b, 0, st, SK_ARGS);
+    else hipLaunchKernelGGL((k_syrk_lower<BN, false, false>), g, b, 0, st, SK_ARGS);
   }
 #undef SK_ARGS
+}
+
+static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
+                        const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
+                        const SyrkEpi& e, const int* info) {
+  if (n <= 0) return;
+  const int64_t T = cdiv(n, 128);
+  if (T * (T + 1) / 2 >= 768)
+    syrk_launch_bn<128>(st, n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e, info);
+  else
+    syrk_launch_bn<64>(st, n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e, info);
 }
 
 void syrk_lower(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
@@ -286,92 +311,36 @@ void syrk_lower(hipStream_t st, int64_t n, int64_t k, double alpha, const double
 
 // =====================================================================================
 // General GEMM update on MFMA:  C(m x n, col-major) -= A(m x k, col-major) B(n x k, col-major)^T
-// (Cholesky sub-panel update).  Same 128x128 tile / 16-deep slab scheme as the SYRK.
-// Operands viewed as "k-major rows": A^T row p = column p of A (contiguous in m).
+// (Cholesky panel / look-ahead updates).  Same tile scheme; operands viewed as k-major rows.
 // =====================================================================================
-template <bool VEC>
-__global__ __launch_bounds__(256, 1) void k_gemm_nt_sub(int64_t m, int64_t n, int64_t K,
-                                                        const double* __restrict__ A, int64_t lda,
-                                                        const double* __restrict__ B, int64_t ldb,
-                                                        double* __restrict__ C, int64_t ldc,
-                                                        const int* __restrict__ info,
-                                                        int64_t tiles_m) {
+template <int BN, bool VEC>
+__global__ __launch_bounds__(256) void k_gemm_nt_sub(int64_t m, int64_t n, int64_t K,
+                                                     const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ B, int64_t ldb,
+                                                     double* __restrict__ C, int64_t ldc,
+                                                     const int* __restrict__ info, int64_t tiles_m) {
+  using T = Tile<BN>;
   if (info && *info != 0) return;
   const int64_t bi = blockIdx.x % tiles_m, bj = blockIdx.x / tiles_m;
-  const int64_t I0 = bi * SK_BN, J0 = bj * SK_BN;
-  __shared__ double sA[2][SK_BK * SK_LDS];
-  __shared__ double sB[2][SK_BK * SK_LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wj = wv >> 1, wi = wv & 1;
-  const int sr = tid >> 4, sc = (tid & 15) * 8;
-  dbl4 acc[4][4];
+  const int64_t I0 = bi * BN, J0 = bj * BN;
+  __shared__ double sA[2 * SK_BK * T::LDS];
+  __shared__ double sB[2 * SK_BK * T::LDS];
+  dbl4 acc[T::TW][T::TW];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < T::TW; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double ra[8], rb[8];
-  auto load_slab = [&](int64_t k0) {
-    const int64_t k = k0 + sr;
-    const bool kin = k < K;
-    const double* ar = A + k * lda;
-    const double* br = B + k * ldb;
-    if (VEC && kin && I0 + sc + 8 <= m && J0 + sc + 8 <= n) {
-      const double2* a2 = reinterpret_cast<const double2*>(ar + I0 + sc);
-      const double2* b2 = reinterpret_cast<const double2*>(br + J0 + sc);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double2 a = a2[q], b = b2[q];
-        ra[2 * q] = a.x; ra[2 * q + 1] = a.y;
-        rb[2 * q] = b.x; rb[2 * q + 1] = b.y;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        ra[q] = (kin && I0 + sc + q < m) ? ar[I0 + sc + q] : 0.0;
-        rb[q] = (kin && J0 + sc + q < n) ? br[J0 + sc + q] : 0.0;
-      }
-    }
-  };
-  auto store_slab = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      sA[buf][sr * SK_LDS + sc + q] = ra[q];
-      sB[buf][sr * SK_LDS + sc + q] = rb[q];
-    }
-  };
-  const int64_t nslab = (K + SK_BK - 1) / SK_BK;
-  if (nslab > 0) { load_slab(0); store_slab(0); }
-  __syncthreads();
+    for (int b = 0; b < T::TW; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  mfma_tile<BN, VEC>(K, I0, J0, m, n, A, lda, B, ldb, nullptr, sA, sB, acc);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wj = wv >> 1, wi = wv & 1;
   const int fr = lane & 15, fk = lane >> 4;
-  for (int64_t s = 0; s < nslab; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nslab) load_slab((s + 1) * SK_BK);
 #pragma unroll
-    for (int kk = 0; kk < SK_BK / 4; ++kk) {
-      const int krow = (kk * 4 + fk) * SK_LDS;
-      double a[4], b[4];
+  for (int tj = 0; tj < T::TW; ++tj)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[t] = sB[buf][krow + wj * 64 + t * 16 + fr];
-        b[t] = sA[buf][krow + wi * 64 + t * 16 + fr];
-      }
-#pragma unroll
-      for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-        for (int ti = 0; ti < 4; ++ti)
-          acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tj], b[ti], acc[tj][ti], 0, 0, 0);
-    }
-    if (s + 1 < nslab) store_slab(buf ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int tj = 0; tj < 4; ++tj)
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti) {
-      const int64_t i = I0 + wi * 64 + ti * 16 + fr;
+    for (int ti = 0; ti < T::TW; ++ti) {
+      const int64_t i = I0 + wi * (BN / 2) + ti * 16 + fr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t j = J0 + wj * 64 + tj * 16 + fk + 4 * r;
+        const int64_t j = J0 + wj * (BN / 2) + tj * 16 + fk + 4 * r;
         if (i < m && j < n) C[j * ldc + i] -= acc[tj][ti][r];
       }
     }
@@ -381,14 +350,19 @@ static void gemm_nt_sub_launch(hipStream_t st, int64_t m, int64_t n, int64_t k, 
                                int64_t lda, const double* B, int64_t ldb, double* C, int64_t ldc,
                                const int* info) {
   if (m <= 0 || n <= 0 || k <= 0) return;
-  const int64_t tm = cdiv(m, SK_BN), tn = cdiv(n, SK_BN);
   bool vec = ((lda & 1) == 0) && ((ldb & 1) == 0) && ((((uintptr_t)A) & 15) == 0) &&
              ((((uintptr_t)B) & 15) == 0);
-  dim3 g(tm * tn), b(256);
-  if (vec)
-    hipLaunchKernelGGL(k_gemm_nt_sub<true>, g, b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
-  else
-    hipLaunchKernelGGL(k_gemm_nt_sub<false>, g, b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
+  const bool big = cdiv(m, 128) * cdiv(n, 128) >= 768;
+  dim3 b(256);
+  if (big) {
+    const int64_t tm = cdiv(m, 128), tn = cdiv(n, 128);
+    if (vec) hipLaunchKernelGGL((k_gemm_nt_sub<128, true>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
+    else hipLaunchKernelGGL((k_gemm_nt_sub<128, false>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
+  } else {
+    const int64_t tm = cdiv(m, 64), tn = cdiv(n, 64);
+    if (vec) hipLaunchKernelGGL((k_gemm_nt_sub<64, true>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
+    else hipLaunchKernelGGL((k_gemm_nt_sub<64, false>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
+  }
 }
 
 void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* A, int64_t lda,
@@ -397,99 +371,235 @@ void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* 
 }
 
 // =====================================================================================
-// Cholesky panel: factor the nb x nb diagonal block and solve the rows below it.
-// Every workgroup factors the diagonal block redundantly in LDS (no inter-workgroup
-// hand-off); workgroup 0 writes L11 back, workgroups g >= 1 each solve 64 rows of
-// L21 = A21 L11^{-T}.  LAPACK potrf failure rule: pivot <= 0 or NaN -> info = column.
+// Cholesky panel (width nb <= 128): factor the nb x nb diagonal block and solve the rows
+// below it.  Every workgroup factors the diagonal block redundantly in LDS (packed lower,
+// 66 KB) -- no inter-workgroup hand-off; workgroup 0 writes L11 back, workgroups g >= 1
+// each solve 64 rows of L21 = A21 L11^{-T}.  LAPACK potrf failure rule: pivot <= 0 or
+// NaN -> info = global column (1-based), first failure wins, later kernels early-exit.
 // =====================================================================================
-constexpr int PF_NB = 64;    // panel width
+constexpr int PF_NB = 128;   // max panel width of one panel kernel
 constexpr int PF_RB = 64;    // rows per workgroup for the TRSM part
 constexpr int PF_LD = PF_NB + 1;
+constexpr int CH_NB = 256;   // outer block (trailing-update depth)
+
+// LDS layout of the panel kernel
+//   diag block (nb <= 128, padded with I to 128): block-packed lower, 16x16 blocks (I >= J),
+//     block (I,J) at bidx(I,J)*256, element (r,c) column-major at c*16 + r      (73.7 KB)
+//   row chunk (64 rows x 128 cols): 8 column blocks, element (r,c) at P*1024 + c*64 + r  (64 KB)
+// f64 MFMA 16x16x4 maps (cdna_hip_programming.md §3): A lane l: A[l&15][l>>4]; B: B[l>>4][l&15];
+// D: D[(l>>4)+4r][l&15].  We compute tile C(i, j) -= sum_p Row(i,p) L(j,p) with a = j, b = i.
+__device__ __forceinline__ int bidx(int I, int J) { return (I * (I + 1)) / 2 + J; }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
 
 __global__ __launch_bounds__(256) void k_potrf_panel(int64_t n, int64_t k0, int nb, double* __restrict__ A,
                                                      int64_t lda, int* __restrict__ info) {
   if (*info != 0) return;
-  __shared__ double sL[PF_NB * PF_LD];
-  __shared__ double sR[PF_RB * PF_LD];
+  __shared__ double sD[36 * 256];
+  __shared__ double sX[8 * 16 * 64];
+  __shared__ double sRinv[16];
   __shared__ int fail;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool has_rows = blockIdx.x > 0;
+  const int64_t r0 = k0 + nb + (int64_t)(blockIdx.x - 1) * PF_RB;
+  const int rows = has_rows ? (int)max((int64_t)0, min((int64_t)PF_RB, n - r0)) : 0;
+  if (has_rows && rows <= 0) return;
   if (tid == 0) fail = 0;
-  // load the diagonal block (lower part) column-major -> sL[i*LD + j] (row i, col j)
-  for (int idx = tid; idx < nb * nb; idx += 256) {
-    const int j = idx / nb, i = idx % nb;
-    sL[i * PF_LD + j] = (i >= j) ? A[(k0 + j) * lda + k0 + i] : 0.0;
+  // ---- load: 16 independent loads in flight per thread, then the LDS stores
+  //   diag block (identity padding beyond nb): element (i, j), thread covers i = tid & 127,
+  //   j = (tid >> 7) + 2 * q  (q = 0..63), lower part only
+  {
+    const int i = tid & 127;
+#pragma unroll
+    for (int qb = 0; qb < 64; qb += 16) {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = (tid >> 7) + 2 * (qb + q);
+        v[q] = (i < nb && j < nb && i >= j) ? A[(k0 + j) * lda + k0 + i] : ((i == j) ? 1.0 : 0.0);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = (tid >> 7) + 2 * (qb + q);
+        if (i >= j) sD[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)] = v[q];
+      }
+    }
+  }
+  if (has_rows) {
+    const int r = tid & 63;
+#pragma unroll
+    for (int qb = 0; qb < 32; qb += 16) {
+      double v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = (tid >> 6) + 4 * (qb + q);
+        v[q] = (r < rows && j < nb) ? A[(k0 + j) * lda + r0 + r] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = (tid >> 6) + 4 * (qb + q);
+        sX[(j >> 4) * 1024 + (j & 15) * 64 + r] = v[q];
+      }
+    }
   }
   __syncthreads();
-  // right-looking factorisation: thread t owns row i = t (t < nb)
-  for (int j = 0; j < nb; ++j) {
-    double djj = sL[j * PF_LD + j];
-    if (!(djj > 0.0)) {  // <= 0 or NaN
-      if (tid == 0) fail = j + 1;
-      break;
+  const int NJ = (nb + 15) >> 4;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int J = 0; J < NJ; ++J) {
+    // ---- 1. left-looking update of block column J (diag blocks I >= J, then the row tiles)
+    if (J > 0) {
+      const int ntile = (8 - J) + (has_rows ? 4 : 0);
+      for (int tI = wv; tI < ntile; tI += 4) {
+        const bool diag_tile = tI < 8 - J;
+        const int I = J + tI;
+        const int T = tI - (8 - J);
+        const int cbase = diag_tile ? bidx(I, J) * 256 + fr : J * 1024 + T * 16 + fr;
+        const int cstride = diag_tile ? 16 : 64;
+        double* cs = diag_tile ? sD : sX;
+        dbl4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = cs[cbase + (fk + 4 * r) * cstride];
+        for (int P = 0; P < J; ++P) {
+          const int abase = bidx(J, P) * 256 + fk * 16 + fr;
+          const int bbase = diag_tile ? bidx(I, P) * 256 + fk * 16 + fr : P * 1024 + fk * 64 + T * 16 + fr;
+          double a[4], b[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            a[s4] = -sD[abase + s4 * 64];
+            b[s4] = cs == sD ? sD[bbase + s4 * 64] : sX[bbase + s4 * 256];
+          }
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[cbase + (fk + 4 * r) * cstride] = acc[r];
+      }
+      __syncthreads();
     }
-    djj = sqrt(djj);
+    // ---- 2. factor the 16x16 diagonal block (J,J) in wave 0 (branch-free, fully unrolled):
+    //         lane r holds row r; broadcasts by readlane; one reciprocal per column
+    if (wv == 0) {
+      double row[16];
+      const int rr = lane & 15;
+      const int db = bidx(J, J) * 256;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
+      int bad = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double piv = readlane_d(row[c], c);
+        if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        const double d = sqrt(piv);
+        const double dinv = 1.0 / d;
+        row[c] = (rr == c) ? d : ((rr > c) ? row[c] * dinv : row[c]);
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) {
+          const double lc2 = readlane_d(row[c], c2);   // L[c2][c]
+          if (rr >= c2) row[c2] -= row[c] * lc2;
+        }
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = (rr >= c) ? row[c] : 0.0;
+        if (lane == 0 && bad) fail = J * 16 + bad;
+        sRinv[rr] = 1.0 / row[rr];
+      }
+    }
     __syncthreads();
-    if (tid == j) sL[j * PF_LD + j] = djj;
-    if (tid > j && tid < nb) sL[tid * PF_LD + j] /= djj;
-    __syncthreads();
-    if (tid > j && tid < nb) {
-      const double lij = sL[tid * PF_LD + j];
-      for (int l = j + 1; l <= tid; ++l) sL[tid * PF_LD + l] -= lij * sL[l * PF_LD + j];
+    if (fail) break;
+    // ---- 3. row solves X L_JJ^T = B for the diag rows below block J and the row chunk
+    {
+      const int nd = (8 - J - 1) * 16;
+      const int tot = nd + (has_rows ? 64 : 0);
+      const int db = bidx(J, J) * 256;
+      for (int t = tid; t < tot; t += 256) {
+        double x[16];
+        double* xs = (t < nd) ? sD : sX;
+        const int base = (t < nd) ? bidx(J + 1 + (t >> 4), J) * 256 + (t & 15) : J * 1024 + (t - nd);
+        const int stride = (t < nd) ? 16 : 64;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) x[c] = xs[base + c * stride];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          double v = x[c];
+#pragma unroll
+          for (int c2 = 0; c2 < c; ++c2) v -= x[c2] * sD[db + c2 * 16 + c];
+          x[c] = v * sRinv[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) xs[base + c * stride] = x[c];
+      }
     }
     __syncthreads();
   }
-  __syncthreads();
   if (fail) {
     if (blockIdx.x == 0 && tid == 0) atomicCAS(info, 0, (int)(k0 + fail));
     return;
   }
-  if (blockIdx.x == 0) {
+  if (!has_rows) {
     for (int idx = tid; idx < nb * nb; idx += 256) {
       const int j = idx / nb, i = idx % nb;
-      if (i >= j) A[(k0 + j) * lda + k0 + i] = sL[i * PF_LD + j];
+      if (i >= j) A[(k0 + j) * lda + k0 + i] = sD[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)];
     }
-    return;
-  }
-  // rows below: r0 = k0 + nb + (g-1)*RB
-  const int64_t r0 = k0 + nb + (int64_t)(blockIdx.x - 1) * PF_RB;
-  const int rows = (int)min((int64_t)PF_RB, n - r0);
-  if (rows <= 0) return;
-  for (int idx = tid; idx < rows * nb; idx += 256) {
-    const int j = idx / rows, r = idx % rows;
-    sR[r * PF_LD + j] = A[(k0 + j) * lda + r0 + r];
-  }
-  __syncthreads();
-  // solve X L11^T = R : thread layout r = tid & 63, column group q = tid >> 6
-  const int r = tid & 63, q = tid >> 6;
-  for (int j = 0; j < nb; ++j) {
-    if (r < rows && q == (j & 3)) sR[r * PF_LD + j] /= sL[j * PF_LD + j];
-    __syncthreads();
-    if (r < rows) {
-      const double xj = sR[r * PF_LD + j];
-      for (int l = j + 1 + ((q - (j + 1)) & 3); l < nb; l += 4) sR[r * PF_LD + l] -= xj * sL[l * PF_LD + j];
+  } else {
+    for (int idx = tid; idx < rows * nb; idx += 256) {
+      const int j = idx / rows, r = idx % rows;
+      A[(k0 + j) * lda + r0 + r] = sX[(j >> 4) * 1024 + (j & 15) * 64 + r];
     }
-    __syncthreads();
   }
-  for (int idx = tid; idx < rows * nb; idx += 256) {
-    const int j = idx / rows, rr = idx % rows;
-    A[(k0 + j) * lda + r0 + rr] = sR[rr * PF_LD + j];
+}
+
+static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info) {
+  const int64_t below = n - k0 - nb;
+  dim3 g(1 + cdiv(std::max<int64_t>(below, 0), PF_RB));
+  hipLaunchKernelGGL(k_potrf_panel, g, dim3(256), 0, st, n, k0, nb, A, lda, info);
+}
+
+// Blocked right-looking Cholesky with one block of look-ahead.
+//   side stream: factor block k (two 128-wide panels + the GEMM between them)
+//   main stream: update block k+1's columns first, release it to the side stream, then the
+//                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
+// Without a side stream (side == main) the same sequence runs in order.
+void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
+                    double* A, int64_t lda, int* info) {
+  hipMemsetAsync(info, 0, sizeof(int), st);
+  const bool two = side != st;
+  if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
+  hipStream_t ps = two ? side : st;
+  for (int64_t k0 = 0; k0 < n; k0 += CH_NB) {
+    const int w = (int)std::min<int64_t>(CH_NB, n - k0);
+    // ---- panel k on the side stream
+    const int w1 = std::min(w, PF_NB);
+    panel_launch(ps, n, k0, w1, A, lda, info);
+    if (w > w1) {
+      // A[k0+w1 : n, k0+w1 : k0+w] -= L[k0+w1 : n, k0 : k0+w1] L[k0+w1 : k0+w, k0 : k0+w1]^T
+      gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
+                         A + (k0 + w1) * lda + k0 + w1, lda, info);
+      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info);
+    }
+    if (two) { hipEventRecord(ev_pan, side); hipStreamWaitEvent(st, ev_pan, 0); }
+    // ---- trailing update on the main stream
+    const int64_t r0 = k0 + w;
+    if (r0 >= n) break;
+    const int64_t w2 = std::min<int64_t>(CH_NB, n - r0);
+    // next block's columns (rectangle; its upper-triangle part is never read)
+    gemm_nt_sub_launch(st, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0, lda,
+                       info);
+    if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
+    if (n - r0 - w2 > 0) {
+      SyrkEpi e;
+      syrk_launch(st, n - r0 - w2, w, -1.0, A + k0 * lda + r0 + w2, lda, nullptr, 0, nullptr, 1.0,
+                  A + (r0 + w2) * lda + r0 + w2, lda, e, info);
+    }
   }
 }
 
 void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info) {
-  hipMemsetAsync(info, 0, sizeof(int), st);
-  for (int64_t k = 0; k < n; k += PF_NB) {
-    const int nb = (int)std::min<int64_t>(PF_NB, n - k);
-    const int64_t below = n - k - nb;
-    dim3 g(1 + cdiv(std::max<int64_t>(below, 0), PF_RB));
-    hipLaunchKernelGGL(k_potrf_panel, g, dim3(256), 0, st, n, k, nb, A, lda, info);
-    if (below > 0) {
-      // trailing update A22 -= L21 L21^T : X = L21^T viewed as k-major rows (col p of L21)
-      SyrkEpi e;
-      syrk_launch(st, below, nb, -1.0, A + k * lda + (k + nb), lda, nullptr, 0, nullptr, 1.0,
-                  A + (k + nb) * lda + (k + nb), lda, e, info);
-    }
-  }
+  potrf_lower_la(st, st, nullptr, nullptr, n, A, lda, info);
 }
 
 // =====================================================================================

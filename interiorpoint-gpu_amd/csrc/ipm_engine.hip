@@ -54,6 +54,8 @@ enum Slot {
 struct ipm_handle {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;        // high-priority stream for Cholesky panels (look-ahead)
+  hipEvent_t ev_rel = nullptr, ev_pan = nullptr;
   bool own_stream = false;
   std::string err;
   double* hbuf = nullptr;  // pinned host staging
@@ -418,6 +420,13 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   // NULL = the legacy default stream (what torch's default stream is), so work is ordered
   // with the caller's tensor initialisation and reads without extra events.
   h->stream = (hipStream_t)stream;
+  {
+    int least = 0, greatest = 0;
+    hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, greatest) != hipSuccess) h->side = nullptr;
+    hipEventCreateWithFlags(&h->ev_rel, hipEventDisableTiming);
+    hipEventCreateWithFlags(&h->ev_pan, hipEventDisableTiming);
+  }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   for (auto& ev : h->ev) hipEventCreate(&ev);
@@ -432,6 +441,9 @@ extern "C" int ipm_destroy(ipm_handle* h) {
   if (h->dinfo) hipFree(h->dinfo);
   if (h->scratch) hipFree(h->scratch);
   for (auto& ev : h->ev) hipEventDestroy(ev);
+  if (h->ev_rel) hipEventDestroy(h->ev_rel);
+  if (h->ev_pan) hipEventDestroy(h->ev_pan);
+  if (h->side) hipStreamDestroy(h->side);
   if (h->own_stream) hipStreamDestroy(h->stream);
   delete h;
   return IPM_OK;
@@ -477,7 +489,7 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
 
 extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info) {
   if (!h || n < 0 || ldh < n) return IPM_INVALID_ARG;
-  potrf_lower(h->stream, n, H, ldh, h->dinfo);
+  potrf_lower_la(h->stream, h->side ? h->side : h->stream, h->ev_rel, h->ev_pan, n, H, ldh, h->dinfo);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;
@@ -826,7 +838,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
   if (!pr->use_backup) {
     ipm_handle* h = pr->h;
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    potrf_lower(st, pr->N, pr->H, pr->ldh, pr->info);
+    potrf_lower_la(st, h->side ? h->side : st, h->ev_rel, h->ev_pan, pr->N, pr->H, pr->ldh, pr->info);
     if (h->timing) hipEventRecord(h->ev[3], st);
     potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2);
   } else {
@@ -873,7 +885,8 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
   const int64_t lds = p + (p & 1);
   if (!pr->use_backup) {
-    potrf_lower(st, pr->N, pr->H, pr->ldh, pr->info);
+    potrf_lower_la(st, pr->h->side ? pr->h->side : st, pr->h->ev_rel, pr->h->ev_pan, pr->N, pr->H, pr->ldh,
+                   pr->info);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
     potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2);
