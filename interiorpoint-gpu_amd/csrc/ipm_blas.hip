@@ -744,9 +744,185 @@ void trsm_lower_bwd(hipStream_t st, int64_t n, int64_t nrhs, const double* L, in
   }
 }
 
-// L L^T X = B in place; W: scratch n x nrhs (ldb)
+// =====================================================================================
+// Single right-hand side (the Newton step of NewtonSolver.py:287-299 / 303-313): each
+// direction is ONE persistent launch.  The solve is HBM-bound (L is read once, 8 n^2/2
+// bytes); its critical path is the chain of 64x64 diagonal-block solves, so everything
+// else is taken off that chain:
+//   * workgroups draw block tickets in solve order (atomic ctl[0]); the owner of block B
+//     streams the off-diagonal tiles of its block row (fwd) / block column (bwd) into
+//     registers one tile AHEAD of the published solutions it multiplies them with,
+//   * the diagonal block is staged in LDS and its reciprocal pivots computed while the
+//     workgroup waits, and the 64-step substitution runs in one wave out of registers
+//     (readlane broadcasts, no barriers),
+//   * the 64 results are published with agent-scope (sc1) stores by that one wave, then
+//     s_waitcnt vmcnt(0), then the progress word ctl[1] = ticket + 1 (sc1).  Consumers poll
+//     the progress word and read the published values with sc1 loads only -- the hand-off
+//     form of MI355X_MICROARCH.md "Valid forms" (no acquire fence on the chain).
+// A workgroup only ever waits on blocks with SMALLER tickets, which are held by running
+// workgroups, so any grid size makes progress; every workgroup exits when tickets run out.
+// Blocks are published in ticket order, so "progress > t" means tickets 0..t are solved.
+// =====================================================================================
+constexpr int TV_B = 64;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_ctl(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double bcast_d(double v, int l) {   // l wave-uniform
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// FWD: solve L y = b.   !FWD: solve L^T y = b.   L column-major lower (ldl); y must not alias b.
+template <bool FWD>
+__global__ __launch_bounds__(256) void k_trsv_chain(int64_t n, int nblk, const double* __restrict__ L,
+                                                    int64_t ldl, const double* __restrict__ b, double* y,
+                                                    unsigned* ctl) {
+  __shared__ double sL[TV_B * (TV_B + 1)];        // diagonal block, column-major, padded
+  __shared__ double sdinv[TV_B];
+  __shared__ double sacc[TV_B * (TV_B + 1)];      // cross-wave / cross-lane partial sums
+  __shared__ int sticket;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (;;) {
+    if (tid == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
+    __syncthreads();
+    const int t = sticket;
+    __syncthreads();
+    if (t >= nblk) break;
+    const int B = FWD ? t : nblk - 1 - t;                 // block this workgroup solves
+    const int64_t r0 = (int64_t)B * TV_B;
+    const int rows = (int)min((int64_t)TV_B, n - r0);
+    const int ntile = t;                                  // tiles from already-solved blocks
+    // ---- off-diagonal tile t' (ticket order): 16 columns per wave, lane = tile row
+    //   FWD: tile L[B, J] with J = t'            -> rows r0.., columns J*64 + w*16 + jj
+    //   BWD: tile L[K, B] with K = nblk-1-t'     -> rows K*64.., columns r0 + w*16 + jj
+    auto load_tile = [&](int tp, double (&dst)[16]) {
+      if (FWD) {
+        const double* base = L + ((int64_t)tp * TV_B + w * 16) * ldl + r0 + lane;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) dst[jj] = lane < rows ? base[jj * ldl] : 0.0;
+      } else {
+        const int64_t k0 = (int64_t)(nblk - 1 - tp) * TV_B;
+        const int krows = (int)min((int64_t)TV_B, n - k0);
+        const double* base = L + (r0 + w * 16) * ldl + k0 + lane;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) dst[jj] = lane < krows ? base[jj * ldl] : 0.0;
+      }
+    };
+    double cur[16], nxt[16];
+    if (ntile > 0) load_tile(0, cur);
+    // stage the diagonal block (lower part) and the reciprocal pivots while tiles stream in
+    for (int idx = tid; idx < TV_B * TV_B; idx += 256) {
+      const int j = idx >> 6, i = idx & 63;
+      sL[j * (TV_B + 1) + i] = (i < rows && j < rows && i >= j) ? L[(r0 + j) * ldl + r0 + i] : 0.0;
+    }
+    __syncthreads();
+    if (tid < TV_B) sdinv[tid] = tid < rows ? 1.0 / sL[tid * (TV_B + 1) + tid] : 0.0;
+    double accf = 0.0;
+    double accb[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) accb[jj] = 0.0;
+    unsigned known = 0;
+    for (int tp = 0; tp < ntile; ++tp) {
+      // poll first, then issue the next tile's loads, then wait only for the poll
+      if (known <= (unsigned)tp) known = ld_ctl(&ctl[1]);
+      if (tp + 1 < ntile) load_tile(tp + 1, nxt);
+      while (known <= (unsigned)tp) {
+        __builtin_amdgcn_s_sleep(1);
+        known = ld_ctl(&ctl[1]);
+      }
+      if (FWD) {
+        // y_J of this wave's 16 columns: wave-uniform sc1 loads (one request each)
+        const double* yj = y + (int64_t)tp * TV_B + w * 16;
+        double v[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) v[jj] = ld_sc1(yj + jj);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) accf = fma(cur[jj], v[jj], accf);
+      } else {
+        const int64_t k0 = (int64_t)(nblk - 1 - tp) * TV_B;
+        const double v = (k0 + lane < n) ? ld_sc1(y + k0 + lane) : 0.0;   // x_K, lane = row
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) accb[jj] = fma(cur[jj], v, accb[jj]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) cur[jj] = nxt[jj];
+    }
+    // ---- reduce the partial sums of the 4 waves (fixed order: deterministic)
+    if (FWD) {
+      sacc[w * (TV_B + 1) + lane] = accf;
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) sacc[(w * 16 + jj) * (TV_B + 1) + lane] = accb[jj];
+    }
+    __syncthreads();
+    if (w == 0) {
+      double s;
+      if (FWD) {
+        s = (sacc[lane] + sacc[(TV_B + 1) + lane]) + (sacc[2 * (TV_B + 1) + lane] + sacc[3 * (TV_B + 1) + lane]);
+      } else {
+        s = 0.0;
+        for (int l = 0; l < TV_B; ++l) s += sacc[lane * (TV_B + 1) + l];
+      }
+      double r = lane < rows ? b[r0 + lane] - s : 0.0;
+      const double dinv = sdinv[lane];
+      // Substitution out of registers.  lv holds the STRICTLY triangular part of the lane's
+      // row (fwd) / column (bwd), so step j leaves lanes <= j (fwd) / >= j (bwd) untouched and
+      // lane j's final value is y_j = r_j * dinv_j -- no per-step lane masks on the chain.
+      double lv[TV_B];
+      if (FWD) {
+        // lane i: L[i][j] (j < i) at sL[j*65 + i]
+#pragma unroll
+        for (int j = 0; j < TV_B; ++j) lv[j] = lane > j ? sL[j * (TV_B + 1) + lane] : 0.0;
+#pragma unroll
+        for (int j = 0; j < TV_B; ++j) r = fma(-lv[j], bcast_d(r * dinv, j), r);
+      } else {
+        // lane k: L[j][k] (j > k) at sL[k*65 + j];  L^T x = r solved for j = 63 .. 0
+#pragma unroll
+        for (int j = 0; j < TV_B; ++j) lv[j] = lane < j ? sL[lane * (TV_B + 1) + j] : 0.0;
+#pragma unroll
+        for (int j = TV_B - 1; j >= 0; --j) r = fma(-lv[j], bcast_d(r * dinv, j), r);
+      }
+      r = r * dinv;
+      if (lane < rows) st_sc1(y + r0 + lane, r);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&ctl[1], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+}
+
+static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int64_t ldl, const double* b,
+                       double* y, unsigned* ctl) {
+  const int nblk = (int)cdiv(n, TV_B);
+  const int grid = std::min(nblk, 1024);
+  if (fwd)
+    hipLaunchKernelGGL(k_trsv_chain<true>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, y, ctl);
+  else
+    hipLaunchKernelGGL(k_trsv_chain<false>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, y, ctl);
+}
+
+// L L^T X = B in place; W: scratch n x nrhs (ldb); ctl: device scratch of 4 words (single
+// right-hand side only; may be null, then the blocked multi-RHS path is used)
 void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W) {
+                 int64_t ldb, double* W, unsigned* ctl) {
+  if (n <= 0 || nrhs <= 0) return;
+  if (nrhs == 1 && ldb == 1 && ctl) {
+    hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned), st);
+    trsv_chain(st, true, n, L, ldl, B, W, ctl);
+    trsv_chain(st, false, n, L, ldl, W, B, ctl + 2);
+    return;
+  }
   trsm_lower_fwd(st, n, nrhs, L, ldl, B, ldb, W);
   trsm_lower_bwd(st, n, nrhs, L, ldl, W, ldb, B);
 }

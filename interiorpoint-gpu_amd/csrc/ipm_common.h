@@ -61,9 +61,10 @@ void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev
 // ev_rel / ev_pan: two events owned by the caller (re-recorded every block)
 void potrf_lower_la(hipStream_t s, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
                     double* H, int64_t ldh, int* info_dev);
-// L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs
+// L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
+// ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W);
+                 int64_t ldb, double* W, unsigned* ctl);
 // forward L Y = B / backward L^T Y = B: B is consumed, the solution goes to Y (same ld)
 void trsm_lower_fwd(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                     int64_t ldb, double* Y);

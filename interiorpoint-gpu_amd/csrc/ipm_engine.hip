@@ -60,6 +60,7 @@ struct ipm_handle {
   std::string err;
   double* hbuf = nullptr;  // pinned host staging
   int* dinfo = nullptr;    // device scratch for level-0 potrf
+  unsigned* ctl = nullptr; // device control words for level-0 potrs
   double* scratch = nullptr;
   size_t scratch_bytes = 0;
   hipEvent_t ev[6];
@@ -98,6 +99,7 @@ struct ipm_problem {
   unsigned long long *pmask = nullptr, *mask = nullptr;
   int64_t *piv = nullptr, *pivp = nullptr;
   int* info = nullptr;
+  unsigned* ctl = nullptr;  // persistent-solve control words
   int64_t part_elems = 0, nls_blocks = 0;
   std::vector<int64_t> rowcone_h, dslot_h;
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
@@ -178,6 +180,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->sums = c.take<double>(NCAND);
   pr->mask = c.take<unsigned long long>(4);
   pr->info = c.take<int>(8);
+  pr->ctl = c.take<unsigned>(8);
   pr->coef = c.take<double>(pr->K + 1);
   pr->ones = c.take<double>(pr->K + 1);
   pr->lhs0 = c.take<double>(pr->Lh + 1);
@@ -429,6 +432,7 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
+  h->ctl = reinterpret_cast<unsigned*>(h->dinfo + 8);
   for (auto& ev : h->ev) hipEventCreate(&ev);
   *out = h;
   return IPM_OK;
@@ -503,7 +507,7 @@ extern "C" int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L
   if (!h || n < 0 || nrhs < 0 || ldl < n || ldb < nrhs) return IPM_INVALID_ARG;
   double* W = scratch(h, std::max<int64_t>(n * ldb, 1) * sizeof(double));
   if (!W) return IPM_HIP_ERROR;
-  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W);
+  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W, h->ctl);
   HIPCHK(h, hipGetLastError());
   return IPM_OK;
 }
@@ -840,7 +844,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
     potrf_lower_la(st, h->side ? h->side : st, h->ev_rel, h->ev_pan, pr->N, pr->H, pr->ldh, pr->info);
     if (h->timing) hipEventRecord(h->ev[3], st);
-    potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2);
+    potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
   } else {
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
     if (rc) return rc;
@@ -874,7 +878,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     mul(st, n, pr->tmpn, pr->g, 1.0, pr->hxs);
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->hxs, 0.0, pr->r2);
     lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
-    potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp);
+    potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp, pr->ctl);
     // dx = (-Hi) * (g + A^T w)
     gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
     lincomb(st, n, 1.0, pr->g, 1.0, pr->ATdv, pr->hxs);
@@ -889,9 +893,9 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
                    pr->info);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
-    potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2);
+    potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
     copy(st, pr->tmpn, pr->g, n);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl);
     // S = A Y (lower)
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
@@ -899,11 +903,11 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     // w = S^-1 (b2 - A hg)
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
     lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
-    potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp);
+    potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp, pr->ctl);
     // dx = -H^-1 (g + A^T w)
     gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
     lincomb(st, n, -1.0, pr->g, -1.0, pr->ATdv, pr->dx);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
     lincomb(st, p, 1.0, pr->wv, -1.0, v, pr->dv);
     return IPM_OK;
   }

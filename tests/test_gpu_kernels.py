@@ -76,3 +76,22 @@ def test_potrf_reports_lapack_info():
     with pytest.raises(np.linalg.LinAlgError) as e:
         scipy.linalg.cho_factor(A)
     assert f"{info}-th leading minor" in str(e.value)
+
+
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 127, 128, 200, 1000, 2049])
+def test_potrs_single_rhs_persistent_solve(n):
+    """nrhs = 1 runs the persistent ticketed solve kernels (k_trsv_chain); partial last block,
+    one block, many blocks."""
+    rng = np.random.default_rng(n + 17)
+    M = rng.normal(size=(n + 3, n))
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 0 and info == 0
+    b = rng.normal(size=n)
+    x = potrs(Hm, n, n, b.copy()).ravel()
+    ref = np.linalg.solve(A, b)
+    np.testing.assert_allclose(x, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+    # repeated calls reuse the control words (reset per call)
+    x2 = potrs(Hm, n, n, b.copy()).ravel()
+    np.testing.assert_array_equal(x, x2)
