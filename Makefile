@@ -12,7 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
             -Wno-unused-variable -Wno-unused-result -Wno-unused-value -Iinclude -I$(SRC_DIR)
 SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
-HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_barrier.h include/ipm355.h
+HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h include/ipm355.h
 
 all: $(OUT)
 

@@ -11,9 +11,11 @@
 // (cuBLAS gemv/gemm via CuPy); NewtonSolver.py:286-313 (cuSOLVER potrf + 2 trsv);
 // NewtonSolverInfeasibleStart.py:398-452 (potrf + trsm with p right-hand sides).
 #include "ipm_common.h"
+#include "ipm_mfma.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace ipm {
 
@@ -127,180 +129,34 @@ void gemv_t(hipStream_t st, int64_t rows, int64_t cols, double alpha, const doub
                      beta, y);
 }
 
-// ---- shared fp64 MFMA tile machinery (SYRK / GEMM)
-constexpr int SK_BK = 16;    // K slab
-// padded LDS row (doubles): BN + 16  -> 2*(BN+16) dwords == 32 mod 64: the two k-rows a
-// wave reads with one ds_read_b64 land in different bank halves (no 2-way conflict)
-template <int BN>
-struct Tile {
-  static constexpr int LDS = BN + 16;
-  static constexpr int TW = BN / 32;              // 16x16 MFMA tiles per wave per dim (2x2 waves)
-  static constexpr int NPT = SK_BK * BN / 256;    // doubles staged per thread per slab
-  static constexpr int TPR = BN / NPT;            // threads per slab row
-};
-
-// Shared MFMA main loop: acc[tj][ti] += sum_k Xw[k][I0+i] * Yv[k][J0+j]
-//   xrow(k) / yrow(k): row pointers (k-major operands), optional weight on the X side.
-template <int BN, bool VEC>
-__device__ __forceinline__ void mfma_tile(int64_t K, int64_t I0, int64_t J0, int64_t ni, int64_t nj,
-                                          const double* __restrict__ X, int64_t ldx,
-                                          const double* __restrict__ Y, int64_t ldy,
-                                          const double* __restrict__ w, double* sX, double* sY,
-                                          dbl4 (&acc)[Tile<BN>::TW][Tile<BN>::TW]) {
-  using T = Tile<BN>;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wj = wv >> 1, wi = wv & 1;
-  const int sr = tid / T::TPR, sc = (tid % T::TPR) * T::NPT;
-  double rx[T::NPT], ry[T::NPT];
-  auto load_slab = [&](int64_t k0) {
-    const int64_t k = k0 + sr;
-    const bool kin = k < K;
-    const double wk = (kin && w) ? w[k] : 1.0;
-    const double* xr = X + k * ldx;
-    const double* yr = Y + k * ldy;
-    if (VEC && kin && I0 + sc + T::NPT <= ni && J0 + sc + T::NPT <= nj) {
-      const double2* x2 = reinterpret_cast<const double2*>(xr + I0 + sc);
-      const double2* y2 = reinterpret_cast<const double2*>(yr + J0 + sc);
-#pragma unroll
-      for (int q = 0; q < T::NPT / 2; ++q) {
-        double2 a = x2[q], b = y2[q];
-        rx[2 * q] = a.x * wk; rx[2 * q + 1] = a.y * wk;
-        ry[2 * q] = b.x; ry[2 * q + 1] = b.y;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < T::NPT; ++q) {
-        const int64_t ci = I0 + sc + q, cj = J0 + sc + q;
-        rx[q] = (kin && ci < ni) ? xr[ci] * wk : 0.0;
-        ry[q] = (kin && cj < nj) ? yr[cj] : 0.0;
-      }
-    }
-  };
-  auto store_slab = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < T::NPT; ++q) {
-      sX[buf * SK_BK * T::LDS + sr * T::LDS + sc + q] = rx[q];
-      sY[buf * SK_BK * T::LDS + sr * T::LDS + sc + q] = ry[q];
-    }
-  };
-  const int64_t nslab = (K + SK_BK - 1) / SK_BK;
-  if (nslab > 0) { load_slab(0); store_slab(0); }
-  __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
-  for (int64_t s = 0; s < nslab; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nslab) load_slab((s + 1) * SK_BK);
-    const double* bx = sX + buf * SK_BK * T::LDS;
-    const double* by = sY + buf * SK_BK * T::LDS;
-#pragma unroll
-    for (int kk = 0; kk < SK_BK / 4; ++kk) {
-      const int krow = (kk * 4 + fk) * T::LDS;
-      double a[T::TW], b[T::TW];
-#pragma unroll
-      for (int t = 0; t < T::TW; ++t) {
-        a[t] = by[krow + wj * (BN / 2) + t * 16 + fr];
-        b[t] = bx[krow + wi * (BN / 2) + t * 16 + fr];
-      }
-#pragma unroll
-      for (int tj = 0; tj < T::TW; ++tj)
-#pragma unroll
-        for (int ti = 0; ti < T::TW; ++ti)
-          acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tj], b[ti], acc[tj][ti], 0, 0, 0);
-    }
-    if (s + 1 < nslab) store_slab(buf ^ 1);
-    __syncthreads();
-  }
-}
-
 // =====================================================================================
-// SYRK / GEMM^T on fp64 MFMA (v_mfma_f64_16x16x4_f64)
-//
+// SYRK / GEMM^T on fp64 MFMA: the tile kernel lives in ipm_mfma.h (k_mfma_gemm).
 //   H(i,j) = alpha * sum_k w[k] X[k][i] Y[k][j] + beta*H(i,j) + tP*P[j][i] + [i==j] dvec[i]
 //   for the lower triangle i >= j; H column-major (element (i,j) at j*ldh + i).
-//
-// BN x BN output tile per 256-thread workgroup (2x2 waves), K staged 16 rows at a time
-// through LDS with a register prefetch of the next slab.  BN = 128 for large grids,
-// 64 when the 128-tile grid would leave CUs idle.
-// f64 MFMA fragment maps (cdna_hip_programming.md §3): A: lane l holds A[l&15][l>>4];
-// B: lane l holds B[l>>4][l&15]; D: lane l holds D[(l>>4)+4r][l&15], r=0..3.
-// j (output column) is the MFMA row and i (output row) the MFMA column, so 16
-// consecutive lanes store 16 consecutive doubles of a column-major H column.
 // =====================================================================================
-template <int BN, bool VEC, bool SYM>
-__global__ __launch_bounds__(256) void k_syrk_lower(
-    int64_t n, int64_t K, double alpha, const double* __restrict__ X, int64_t ldx,
-    const double* __restrict__ Y, int64_t ldy, const double* __restrict__ w, double beta,
-    double* __restrict__ H, int64_t ldh, const double* __restrict__ P, int64_t ldp, double tP,
-    const double* __restrict__ dvec, const int* __restrict__ info, int64_t tiles_n) {
-  using T = Tile<BN>;
-  if (info && *info != 0) return;
-  const int64_t L = blockIdx.x;
-  int64_t bi = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= L) ++bi;
-  while (bi * (bi + 1) / 2 > L) --bi;
-  const int64_t bj = L - bi * (bi + 1) / 2;
-  const int64_t I0 = bi * BN, J0 = bj * BN;
-  __shared__ double sX[2 * SK_BK * T::LDS];
-  __shared__ double sY[2 * SK_BK * T::LDS];
-  dbl4 acc[T::TW][T::TW];
-#pragma unroll
-  for (int a = 0; a < T::TW; ++a)
-#pragma unroll
-    for (int b = 0; b < T::TW; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  mfma_tile<BN, VEC>(K, I0, J0, n, n, X, ldx, SYM ? X : Y, SYM ? ldx : ldy, w, sX, sY, acc);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wj = wv >> 1, wi = wv & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-#pragma unroll
-  for (int tj = 0; tj < T::TW; ++tj) {
-#pragma unroll
-    for (int ti = 0; ti < T::TW; ++ti) {
-      const int64_t i = I0 + wi * (BN / 2) + ti * 16 + fr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t j = J0 + wj * (BN / 2) + tj * 16 + fk + 4 * r;
-        if (i < n && j < n && i >= j) {
-          double v = alpha * acc[tj][ti][r];
-          double* hp = H + j * ldh + i;
-          if (beta != 0.0) v += beta * (*hp);
-          if (P) v += tP * P[j * ldp + i];
-          if (dvec && i == j) v += dvec[i];
-          *hp = v;
-        }
-      }
-    }
-  }
-}
-
-template <int BN>
-static void syrk_launch_bn(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
-                           const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
-                           const SyrkEpi& e, const int* info) {
-  const int64_t T = cdiv(n, BN);
-  const int64_t nblk = T * (T + 1) / 2;
-  const bool sym = (Y == nullptr) || (Y == X && ldy == ldx);
-  bool vec = ((ldx & 1) == 0) && ((((uintptr_t)X) & 15) == 0);
-  if (!sym) vec = vec && ((ldy & 1) == 0) && ((((uintptr_t)Y) & 15) == 0);
-  dim3 g(nblk), b(256);
-#define SK_ARGS n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e.P, e.ldp, e.tP, e.dvec, info, T
-  if (sym) {
-    if (vec) hipLaunchKernelGGL((k_syrk_lower<BN, true, true>), g, b, 0, st, SK_ARGS);
-    else hipLaunchKernelGGL((k_syrk_lower<BN, false, true>), g, b, 0, st, SK_ARGS);
-  } else {
-    if (vec) hipLaunchKernelGGL((k_syrk_lower<BN, true, false>), g, b, 0, st, SK_ARGS);
-    else hipLaunchKernelGGL((k_syrk_lower<BN, false, false>), g, b, 0, st, SK_ARGS);
-  }
-#undef SK_ARGS
-}
-
 static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
                         const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
                         const SyrkEpi& e, const int* info) {
   if (n <= 0) return;
-  const int64_t T = cdiv(n, 128);
-  if (T * (T + 1) / 2 >= 768)
-    syrk_launch_bn<128>(st, n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e, info);
-  else
-    syrk_launch_bn<64>(st, n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, e, info);
+  GemmArgs a;
+  a.ni = a.nj = n;
+  a.K = k;
+  a.X = X;
+  a.ldx = ldx;
+  a.Y = Y ? Y : X;
+  a.ldy = Y ? ldy : ldx;
+  a.w = w;
+  a.C = H;
+  a.ldc = ldh;
+  a.alpha = alpha;
+  a.beta = beta;
+  a.P = e.P;
+  a.ldp = e.ldp;
+  a.tP = e.tP;
+  a.dvec = e.dvec;
+  a.info = info;
+  a.tri = 1;
+  mfma_gemm_launch(st, a);
 }
 
 void syrk_lower(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
@@ -309,60 +165,24 @@ void syrk_lower(hipStream_t st, int64_t n, int64_t k, double alpha, const double
   syrk_launch(st, n, k, alpha, X, ldx, Y, ldy, w, beta, H, ldh, epi, nullptr);
 }
 
-// =====================================================================================
-// General GEMM update on MFMA:  C(m x n, col-major) -= A(m x k, col-major) B(n x k, col-major)^T
-// (Cholesky panel / look-ahead updates).  Same tile scheme; operands viewed as k-major rows.
-// =====================================================================================
-template <int BN, bool VEC>
-__global__ __launch_bounds__(256) void k_gemm_nt_sub(int64_t m, int64_t n, int64_t K,
-                                                     const double* __restrict__ A, int64_t lda,
-                                                     const double* __restrict__ B, int64_t ldb,
-                                                     double* __restrict__ C, int64_t ldc,
-                                                     const int* __restrict__ info, int64_t tiles_m) {
-  using T = Tile<BN>;
-  if (info && *info != 0) return;
-  const int64_t bi = blockIdx.x % tiles_m, bj = blockIdx.x / tiles_m;
-  const int64_t I0 = bi * BN, J0 = bj * BN;
-  __shared__ double sA[2 * SK_BK * T::LDS];
-  __shared__ double sB[2 * SK_BK * T::LDS];
-  dbl4 acc[T::TW][T::TW];
-#pragma unroll
-  for (int a = 0; a < T::TW; ++a)
-#pragma unroll
-    for (int b = 0; b < T::TW; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  mfma_tile<BN, VEC>(K, I0, J0, m, n, A, lda, B, ldb, nullptr, sA, sB, acc);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wj = wv >> 1, wi = wv & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-#pragma unroll
-  for (int tj = 0; tj < T::TW; ++tj)
-#pragma unroll
-    for (int ti = 0; ti < T::TW; ++ti) {
-      const int64_t i = I0 + wi * (BN / 2) + ti * 16 + fr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t j = J0 + wj * (BN / 2) + tj * 16 + fk + 4 * r;
-        if (i < m && j < n) C[j * ldc + i] -= acc[tj][ti][r];
-      }
-    }
-}
-
+// C(m x n, col-major) -= A(m x k, col-major) B(n x k, col-major)^T   (Cholesky panel / look-ahead)
 static void gemm_nt_sub_launch(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* A,
                                int64_t lda, const double* B, int64_t ldb, double* C, int64_t ldc,
                                const int* info) {
   if (m <= 0 || n <= 0 || k <= 0) return;
-  bool vec = ((lda & 1) == 0) && ((ldb & 1) == 0) && ((((uintptr_t)A) & 15) == 0) &&
-             ((((uintptr_t)B) & 15) == 0);
-  const bool big = cdiv(m, 128) * cdiv(n, 128) >= 768;
-  dim3 b(256);
-  if (big) {
-    const int64_t tm = cdiv(m, 128), tn = cdiv(n, 128);
-    if (vec) hipLaunchKernelGGL((k_gemm_nt_sub<128, true>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
-    else hipLaunchKernelGGL((k_gemm_nt_sub<128, false>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
-  } else {
-    const int64_t tm = cdiv(m, 64), tn = cdiv(n, 64);
-    if (vec) hipLaunchKernelGGL((k_gemm_nt_sub<64, true>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
-    else hipLaunchKernelGGL((k_gemm_nt_sub<64, false>), dim3(tm * tn), b, 0, st, m, n, k, A, lda, B, ldb, C, ldc, info, tm);
-  }
+  GemmArgs a;
+  a.ni = m;
+  a.nj = n;
+  a.K = k;
+  a.X = A;
+  a.ldx = lda;
+  a.Y = B;
+  a.ldy = ldb;
+  a.C = C;
+  a.ldc = ldc;
+  a.info = info;
+  a.sub = 1;
+  mfma_gemm_launch(st, a);
 }
 
 void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* A, int64_t lda,
@@ -371,23 +191,27 @@ void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* 
 }
 
 // =====================================================================================
-// Cholesky panel (width nb <= 128): factor the nb x nb diagonal block and solve the rows
-// below it.  Every workgroup factors the diagonal block redundantly in LDS (packed lower,
-// 66 KB) -- no inter-workgroup hand-off; workgroup 0 writes L11 back, workgroups g >= 1
-// each solve 64 rows of L21 = A21 L11^{-T}.  LAPACK potrf failure rule: pivot <= 0 or
-// NaN -> info = global column (1-based), first failure wins, later kernels early-exit.
+// Cholesky panel (width nb <= 128) in two launches, no redundant work:
+//   k_potrf_diag : ONE workgroup factors the nb x nb diagonal block in LDS (16 x 16 blocks,
+//                  left-looking, MFMA block updates), writes L11 in place and the inverses
+//                  of its eight 16 x 16 diagonal blocks Dinv_J = L_JJ^-1 to a workspace.
+//   k_potrf_trsm : rows below the block, L21 = A21 L11^-T, 64 rows per workgroup, 16 rows
+//                  per wave.  Each wave runs the 8-step block forward substitution entirely in
+//                  MFMA registers: X_J = (B_J - sum_{P<J} X_P L_JP^T) Dinv_J^T.
+// LAPACK potrf failure rule: pivot <= 0 or NaN -> info = global column (1-based), first
+// failure wins; every later kernel of the factorisation early-exits on *info != 0.
+// f64 MFMA 16x16x4 maps (cdna_hip_programming.md §3): A lane l: A[l&15][l>>4];
+// B lane l: B[l>>4][l&15]; D lane l, reg r: D[(l>>4)+4r][l&15].  All tiles are kept
+// TRANSPOSED (D[j][i] = T[i][j]): then 16 consecutive lanes hold 16 consecutive rows of a
+// column-major tile, and the accumulator registers of one product are directly the B
+// operands (k-steps s = r) of the next one -- no shuffles or LDS round trips on the chains.
 // =====================================================================================
-constexpr int PF_NB = 128;   // max panel width of one panel kernel
-constexpr int PF_RB = 64;    // rows per workgroup for the TRSM part
-constexpr int PF_LD = PF_NB + 1;
+constexpr int PF_NB = 128;   // panel width
+constexpr int PF_RB = 64;    // rows per TRSM workgroup
 constexpr int CH_NB = 256;   // outer block (trailing-update depth)
+constexpr int PF_WS = 8 * 256;   // doubles of workspace: the eight Dinv blocks
 
-// LDS layout of the panel kernel
-//   diag block (nb <= 128, padded with I to 128): block-packed lower, 16x16 blocks (I >= J),
-//     block (I,J) at bidx(I,J)*256, element (r,c) column-major at c*16 + r      (73.7 KB)
-//   row chunk (64 rows x 128 cols): 8 column blocks, element (r,c) at P*1024 + c*64 + r  (64 KB)
-// f64 MFMA 16x16x4 maps (cdna_hip_programming.md §3): A lane l: A[l&15][l>>4]; B: B[l>>4][l&15];
-// D: D[(l>>4)+4r][l&15].  We compute tile C(i, j) -= sum_p Row(i,p) L(j,p) with a = j, b = i.
+// packed lower 16x16-block storage: block (I,J), I >= J, at bidx(I,J)*256, element (r,c) at c*16+r
 __device__ __forceinline__ int bidx(int I, int J) { return (I * (I + 1)) / 2 + J; }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -396,167 +220,259 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(256) void k_potrf_panel(int64_t n, int64_t k0, int nb, double* __restrict__ A,
-                                                     int64_t lda, int* __restrict__ info) {
+#ifdef IPM_STAMPS
+__device__ unsigned long long ipm_stamps[64];
+#define STAMP() do { if (tid == 0) ipm_stamps[nst] = __builtin_amdgcn_s_memtime(); ++nst; } while (0)
+#else
+#define STAMP() do {} while (0)
+#endif
+
+// LDS footprint 74 KB and <= 128 VGPRs: the kernel fits on a CU beside one trailing-update
+// workgroup (k_mfma_gemm: 73.7 KB, 200 VGPRs), so the look-ahead stream is not starved.
+__global__ __launch_bounds__(512) void k_potrf_diag(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
+                                                    double* __restrict__ dinv_out, int* __restrict__ info) {
   if (*info != 0) return;
-  __shared__ double sD[36 * 256];
-  __shared__ double sX[8 * 16 * 64];
-  __shared__ double sRinv[16];
+  __shared__ double sD[36 * 256];   // L11 (identity-padded beyond nb)
+  __shared__ double sI[256];        // Dinv_J of the current block column
+  __shared__ double srinv[16];      // 1 / L_cc of the current diagonal block
+  __shared__ double sLr[256];       // L_JJ row-major
   __shared__ int fail;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const bool has_rows = blockIdx.x > 0;
-  const int64_t r0 = k0 + nb + (int64_t)(blockIdx.x - 1) * PF_RB;
-  const int rows = has_rows ? (int)max((int64_t)0, min((int64_t)PF_RB, n - r0)) : 0;
-  if (has_rows && rows <= 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 8 waves
+  const int fr = lane & 15, fk = lane >> 4;
+#ifdef IPM_STAMPS
+  int nst = 0;
+#endif
   if (tid == 0) fail = 0;
-  // ---- load: 16 independent loads in flight per thread, then the LDS stores
-  //   diag block (identity padding beyond nb): element (i, j), thread covers i = tid & 127,
-  //   j = (tid >> 7) + 2 * q  (q = 0..63), lower part only
+  STAMP();
+  // ---- load the lower 128 x 128: thread -> rows (2 i2, 2 i2 + 1), columns j = (tid >> 6) + 8q;
+  //      all 16 loads in flight together, branch-free (clamped addresses, selects afterwards)
+  const int i0 = 2 * (tid & 63), jb = tid >> 6;
   {
+    const bool vec = ((lda & 1) == 0) && ((k0 & 1) == 0);
+    const int ic0 = min(i0, nb - 1), ic1 = min(i0 + 1, nb - 1);
+    const double* base = A + k0 * lda + k0;
+    double2 v[16];
+    if (vec && i0 + 1 < nb) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int jc = min(jb + 8 * q, nb - 1);
+        v[q] = *reinterpret_cast<const double2*>(base + jc * lda + i0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int jc = min(jb + 8 * q, nb - 1);
+        v[q].x = base[jc * lda + ic0];
+        v[q].y = base[jc * lda + ic1];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = jb + 8 * q;
+      if ((i0 >> 4) >= (j >> 4)) {
+        double2 u;
+        u.x = (i0 < j) ? 0.0 : ((i0 < nb && j < nb) ? v[q].x : (i0 == j ? 1.0 : 0.0));
+        u.y = (i0 + 1 < j) ? 0.0 : ((i0 + 1 < nb && j < nb) ? v[q].y : (i0 + 1 == j ? 1.0 : 0.0));
+        *reinterpret_cast<double2*>(&sD[bidx(i0 >> 4, j >> 4) * 256 + (j & 15) * 16 + (i0 & 15)]) = u;
+      }
+    }
+  }
+  __syncthreads();
+  STAMP();
+  for (int J = 0; J < 8; ++J) {
+    // ---- 1. left-looking update of block column J: T_IJ -= sum_{P<J} L_IP L_JP^T, I >= J
+    if (J > 0 && wv < 8 - J) {
+      const int I = J + wv;
+      const int cb = bidx(I, J) * 256 + fk * 16 + fr;
+      dbl4 acc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[0][r] = sD[cb + 64 * r];
+      for (int P = 0; P < J; ++P) {
+        const int ab = bidx(J, P) * 256 + fk * 16 + fr, bb = bidx(I, P) * 256 + fk * 16 + fr;
+        double av[4], bv[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          av[s4] = -sD[ab + 64 * s4];
+          bv[s4] = sD[bb + 64 * s4];
+        }
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[s4], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+    }
+    __syncthreads();
+    STAMP();
+    // ---- 2. wave 0: factor the 16 x 16 block (J,J) in registers (lane r = row r), then its
+    //         inverse (lane c = column c of L_JJ^-1, forward substitution with broadcast LDS
+    //         reads of L and the reciprocal pivots)
+    if (wv == 0) {
+      const int db = bidx(J, J) * 256;
+      const int rr = lane & 15;
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
+      // Right-looking, NO lane masks: entries above the diagonal (lane r < column c) turn into
+      // garbage but are never read -- every broadcast below reads lane c2 > c or the pivot lane.
+      int bad = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double piv = readlane_d(row[c], c);
+        if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        const double dv = rsqrt(piv);      // 1 / L_cc   (sqrt and reciprocal off one chain)
+        row[c] *= dv;                      // lane c: piv * dv = L_cc
+        if (lane == c) srinv[c] = dv;
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) row[c2] = fma(-row[c], readlane_d(row[c], c2), row[c2]);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const double v = (rr >= c) ? row[c] : 0.0;
+          sD[db + c * 16 + rr] = v;          // column-major block
+          sLr[rr * 16 + c] = v;              // row-major copy for the broadcast reads below
+        }
+      }
+      if (lane == 0 && bad) fail = J * 16 + bad;
+      STAMP();
+      // inverse X = L^-1: lane c computes column c, X[r][c] = (d_rc - sum_{k<r} L[r][k] X[k][c]) / L_rr
+      const int c = lane & 15;
+      double x[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < r; ++k) v = fma(-sLr[r * 16 + k], x[k], v);
+        x[r] = (r >= c) ? v * srinv[r] : 0.0;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sI[c * 16 + r] = x[r];
+          dinv_out[J * 256 + c * 16 + r] = x[r];
+        }
+      }
+    }
+    __syncthreads();
+    STAMP();
+    if (fail) break;
+    // ---- 3. L_IJ = T_IJ Dinv_J^T for I > J:  D[j][i] = sum_k Dinv[j][k] T[i][k]
+    if (wv < 7 - J) {
+      const int I = J + 1 + wv;
+      const int cb = bidx(I, J) * 256 + fk * 16 + fr;
+      const int ib = fk * 16 + fr;
+      double bv[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) bv[s4] = sD[cb + 64 * s4];
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sI[ib + 64 * s4], bv[s4], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = acc[r];
+    }
+    __syncthreads();
+    STAMP();
+  }
+  if (fail) {
+    if (tid == 0) atomicCAS(info, 0, (int)(k0 + fail));
+    return;
+  }
+  // ---- write back L11 (lower part, i < nb, j < nb)
+  {
+    double* col = A + k0 * lda + k0 + i0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = jb + 8 * q;
+      if ((i0 >> 4) >= (j >> 4) && j < nb) {
+        const double2 v = *reinterpret_cast<const double2*>(&sD[bidx(i0 >> 4, j >> 4) * 256 + (j & 15) * 16 + (i0 & 15)]);
+        if (i0 >= j && i0 < nb) col[j * lda] = v.x;
+        if (i0 + 1 >= j && i0 + 1 < nb) col[j * lda + 1] = v.y;
+      }
+    }
+  }
+  STAMP();
+}
+#undef STAMP
+
+__global__ __launch_bounds__(256) void k_potrf_trsm(int64_t n, int64_t k0, int nb, double* __restrict__ A,
+                                                    int64_t lda, const double* __restrict__ dinv,
+                                                    const int* __restrict__ info) {
+  if (*info != 0) return;
+  __shared__ double sL[36 * 256];   // off-diagonal blocks of L11 at bidx (I > J); Dinv_J at bidx(J,J)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int64_t row0 = k0 + nb + (int64_t)blockIdx.x * PF_RB + wv * 16;
+  const int64_t row = row0 + fr;
+  const bool rin = row < n;
+  // prefetch this wave's 16 x 128 slab of A21 (transposed D layout): acc_J reg r = B[row][J*16 + fk + 4r]
+  double b[8][4];
+#pragma unroll
+  for (int J = 0; J < 8; ++J)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = J * 16 + fk + 4 * r;
+      b[J][r] = (rin && c < nb) ? A[(k0 + c) * lda + row] : 0.0;
+    }
+  // stage L11 (identity-padded like the diagonal kernel) and Dinv
+  {
+    // thread: row i = tid & 127 of columns j = (tid >> 7) + 2q; strictly-lower blocks only; loads in
+    // batches of 16 so they are in flight together
     const int i = tid & 127;
+    const double* col = A + k0 * lda + k0 + i;
 #pragma unroll
     for (int qb = 0; qb < 64; qb += 16) {
       double v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int j = (tid >> 7) + 2 * (qb + q);
-        v[q] = (i < nb && j < nb && i >= j) ? A[(k0 + j) * lda + k0 + i] : ((i == j) ? 1.0 : 0.0);
+        v[q] = ((i >> 4) > (j >> 4) && i < nb && j < nb) ? col[j * lda] : 0.0;
       }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int j = (tid >> 7) + 2 * (qb + q);
-        if (i >= j) sD[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)] = v[q];
+        if ((i >> 4) > (j >> 4)) sL[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)] = v[q];
       }
     }
   }
-  if (has_rows) {
-    const int r = tid & 63;
-#pragma unroll
-    for (int qb = 0; qb < 32; qb += 16) {
-      double v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = (tid >> 6) + 4 * (qb + q);
-        v[q] = (r < rows && j < nb) ? A[(k0 + j) * lda + r0 + r] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = (tid >> 6) + 4 * (qb + q);
-        sX[(j >> 4) * 1024 + (j & 15) * 64 + r] = v[q];
-      }
-    }
-  }
+  for (int idx = tid; idx < 8 * 256; idx += 256) sL[bidx(idx >> 8, idx >> 8) * 256 + (idx & 255)] = dinv[idx];
   __syncthreads();
-  const int NJ = (nb + 15) >> 4;
-  const int fr = lane & 15, fk = lane >> 4;
-  for (int J = 0; J < NJ; ++J) {
-    // ---- 1. left-looking update of block column J (diag blocks I >= J, then the row tiles)
-    if (J > 0) {
-      const int ntile = (8 - J) + (has_rows ? 4 : 0);
-      for (int tI = wv; tI < ntile; tI += 4) {
-        const bool diag_tile = tI < 8 - J;
-        const int I = J + tI;
-        const int T = tI - (8 - J);
-        const int cbase = diag_tile ? bidx(I, J) * 256 + fr : J * 1024 + T * 16 + fr;
-        const int cstride = diag_tile ? 16 : 64;
-        double* cs = diag_tile ? sD : sX;
-        dbl4 acc;
+  dbl4 x[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = cs[cbase + (fk + 4 * r) * cstride];
-        for (int P = 0; P < J; ++P) {
-          const int abase = bidx(J, P) * 256 + fk * 16 + fr;
-          const int bbase = diag_tile ? bidx(I, P) * 256 + fk * 16 + fr : P * 1024 + fk * 64 + T * 16 + fr;
-          double a[4], b[4];
+  for (int J = 0; J < 8; ++J) {
+    dbl4 acc = dbl4{b[J][0], b[J][1], b[J][2], b[J][3]};
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            a[s4] = -sD[abase + s4 * 64];
-            b[s4] = cs == sD ? sD[bbase + s4 * 64] : sX[bbase + s4 * 256];
-          }
+    for (int P = 0; P < J; ++P) {
+      const int ab = bidx(J, P) * 256 + fk * 16 + fr;
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cs[cbase + (fk + 4 * r) * cstride] = acc[r];
-      }
-      __syncthreads();
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-sL[ab + 64 * s4], x[P][s4], acc, 0, 0, 0);
     }
-    // ---- 2. factor the 16x16 diagonal block (J,J) in wave 0 (branch-free, fully unrolled):
-    //         lane r holds row r; broadcasts by readlane; one reciprocal per column
-    if (wv == 0) {
-      double row[16];
-      const int rr = lane & 15;
-      const int db = bidx(J, J) * 256;
+    const int ib = bidx(J, J) * 256 + fk * 16 + fr;
+    dbl4 xj = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
-      int bad = 0;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d(row[c], c);
-        if (!(piv > 0.0) && bad == 0) bad = c + 1;
-        const double d = sqrt(piv);
-        const double dinv = 1.0 / d;
-        row[c] = (rr == c) ? d : ((rr > c) ? row[c] * dinv : row[c]);
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) {
-          const double lc2 = readlane_d(row[c], c2);   // L[c2][c]
-          if (rr >= c2) row[c2] -= row[c] * lc2;
-        }
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = (rr >= c) ? row[c] : 0.0;
-        if (lane == 0 && bad) fail = J * 16 + bad;
-        sRinv[rr] = 1.0 / row[rr];
-      }
-    }
-    __syncthreads();
-    if (fail) break;
-    // ---- 3. row solves X L_JJ^T = B for the diag rows below block J and the row chunk
-    {
-      const int nd = (8 - J - 1) * 16;
-      const int tot = nd + (has_rows ? 64 : 0);
-      const int db = bidx(J, J) * 256;
-      for (int t = tid; t < tot; t += 256) {
-        double x[16];
-        double* xs = (t < nd) ? sD : sX;
-        const int base = (t < nd) ? bidx(J + 1 + (t >> 4), J) * 256 + (t & 15) : J * 1024 + (t - nd);
-        const int stride = (t < nd) ? 16 : 64;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) x[c] = xs[base + c * stride];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          double v = x[c];
-#pragma unroll
-          for (int c2 = 0; c2 < c; ++c2) v -= x[c2] * sD[db + c2 * 16 + c];
-          x[c] = v * sRinv[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 16; ++c) xs[base + c * stride] = x[c];
-      }
-    }
-    __syncthreads();
+    for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(sL[ib + 64 * s4], acc[s4], xj, 0, 0, 0);
+    x[J] = xj;
   }
-  if (fail) {
-    if (blockIdx.x == 0 && tid == 0) atomicCAS(info, 0, (int)(k0 + fail));
-    return;
-  }
-  if (!has_rows) {
-    for (int idx = tid; idx < nb * nb; idx += 256) {
-      const int j = idx / nb, i = idx % nb;
-      if (i >= j) A[(k0 + j) * lda + k0 + i] = sD[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)];
-    }
-  } else {
-    for (int idx = tid; idx < rows * nb; idx += 256) {
-      const int j = idx / rows, r = idx % rows;
-      A[(k0 + j) * lda + r0 + r] = sX[(j >> 4) * 1024 + (j & 15) * 64 + r];
-    }
+  if (rin) {
+#pragma unroll
+    for (int J = 0; J < 8; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = J * 16 + fk + 4 * r;
+        if (c < nb) A[(k0 + c) * lda + row] = x[J][r];
+      }
   }
 }
 
-static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info) {
+// one panel of width nb <= 128 at column k0: diagonal block, then the rows below it
+static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info,
+                         double* ws) {
+  hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(512), 0, st, k0, nb, A, lda, ws, info);
   const int64_t below = n - k0 - nb;
-  dim3 g(1 + cdiv(std::max<int64_t>(below, 0), PF_RB));
-  hipLaunchKernelGGL(k_potrf_panel, g, dim3(256), 0, st, n, k0, nb, A, lda, info);
+  if (below > 0)
+    hipLaunchKernelGGL(k_potrf_trsm, dim3(cdiv(below, PF_RB)), dim3(256), 0, st, n, k0, nb, A, lda,
+                       (const double*)ws, (const int*)info);
 }
 
 // Blocked right-looking Cholesky with one block of look-ahead.
@@ -565,7 +481,7 @@ static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* 
 //                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
 // Without a side stream (side == main) the same sequence runs in order.
 void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
-                    double* A, int64_t lda, int* info) {
+                    double* A, int64_t lda, int* info, double* ws) {
   hipMemsetAsync(info, 0, sizeof(int), st);
   const bool two = side != st;
   if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
@@ -574,12 +490,12 @@ void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEven
     const int w = (int)std::min<int64_t>(CH_NB, n - k0);
     // ---- panel k on the side stream
     const int w1 = std::min(w, PF_NB);
-    panel_launch(ps, n, k0, w1, A, lda, info);
+    panel_launch(ps, n, k0, w1, A, lda, info, ws);
     if (w > w1) {
       // A[k0+w1 : n, k0+w1 : k0+w] -= L[k0+w1 : n, k0 : k0+w1] L[k0+w1 : k0+w, k0 : k0+w1]^T
       gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
                          A + (k0 + w1) * lda + k0 + w1, lda, info);
-      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info);
+      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws);
     }
     if (two) { hipEventRecord(ev_pan, side); hipStreamWaitEvent(st, ev_pan, 0); }
     // ---- trailing update on the main stream
@@ -598,8 +514,8 @@ void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEven
   }
 }
 
-void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info) {
-  potrf_lower_la(st, st, nullptr, nullptr, n, A, lda, info);
+void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
+  potrf_lower_la(st, st, nullptr, nullptr, n, A, lda, info, ws);
 }
 
 // =====================================================================================

@@ -56,11 +56,13 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
                  const double* B, int64_t ldb, double* C, int64_t ldc);
 
 // Cholesky (column-major lower, in place). info_dev: device int (0 or first failing column, 1-based)
-void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev);
+// ws: device workspace of POTRF_WS_DOUBLES doubles (the panel's inverted diagonal blocks)
+constexpr int64_t POTRF_WS_DOUBLES = 8 * 256;
+void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
 // same with one block of look-ahead: panels on `side` (high priority), trailing updates on `s`;
 // ev_rel / ev_pan: two events owned by the caller (re-recorded every block)
 void potrf_lower_la(hipStream_t s, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
-                    double* H, int64_t ldh, int* info_dev);
+                    double* H, int64_t ldh, int* info_dev, double* ws);
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,

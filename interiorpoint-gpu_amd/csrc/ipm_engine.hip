@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -61,6 +62,7 @@ struct ipm_handle {
   double* hbuf = nullptr;  // pinned host staging
   int* dinfo = nullptr;    // device scratch for level-0 potrf
   unsigned* ctl = nullptr; // device control words for level-0 potrs
+  double* pws = nullptr;   // device workspace for level-0 potrf
   double* scratch = nullptr;
   size_t scratch_bytes = 0;
   hipEvent_t ev[6];
@@ -100,6 +102,7 @@ struct ipm_problem {
   int64_t *piv = nullptr, *pivp = nullptr;
   int* info = nullptr;
   unsigned* ctl = nullptr;  // persistent-solve control words
+  double* pws = nullptr;    // Cholesky panel workspace (inverted diagonal blocks)
   int64_t part_elems = 0, nls_blocks = 0;
   std::vector<int64_t> rowcone_h, dslot_h;
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
@@ -181,6 +184,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->mask = c.take<unsigned long long>(4);
   pr->info = c.take<int>(8);
   pr->ctl = c.take<unsigned>(8);
+  pr->pws = c.take<double>(POTRF_WS_DOUBLES);
   pr->coef = c.take<double>(pr->K + 1);
   pr->ones = c.take<double>(pr->K + 1);
   pr->lhs0 = c.take<double>(pr->Lh + 1);
@@ -426,13 +430,16 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   {
     int least = 0, greatest = 0;
     hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, greatest) != hipSuccess) h->side = nullptr;
+    const char* nola = getenv("IPM_NO_LOOKAHEAD");   // debug: run the Cholesky on one stream
+    if (nola && nola[0] == '1') h->side = nullptr;
+    else if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, greatest) != hipSuccess) h->side = nullptr;
     hipEventCreateWithFlags(&h->ev_rel, hipEventDisableTiming);
     hipEventCreateWithFlags(&h->ev_pan, hipEventDisableTiming);
   }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   h->ctl = reinterpret_cast<unsigned*>(h->dinfo + 8);
+  if (hipMalloc((void**)&h->pws, POTRF_WS_DOUBLES * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   for (auto& ev : h->ev) hipEventCreate(&ev);
   *out = h;
   return IPM_OK;
@@ -443,6 +450,7 @@ extern "C" int ipm_destroy(ipm_handle* h) {
   hipStreamSynchronize(h->stream);
   if (h->hbuf) hipHostFree(h->hbuf);
   if (h->dinfo) hipFree(h->dinfo);
+  if (h->pws) hipFree(h->pws);
   if (h->scratch) hipFree(h->scratch);
   for (auto& ev : h->ev) hipEventDestroy(ev);
   if (h->ev_rel) hipEventDestroy(h->ev_rel);
@@ -493,7 +501,7 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
 
 extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info) {
   if (!h || n < 0 || ldh < n) return IPM_INVALID_ARG;
-  potrf_lower_la(h->stream, h->side ? h->side : h->stream, h->ev_rel, h->ev_pan, n, H, ldh, h->dinfo);
+  potrf_lower_la(h->stream, h->side ? h->side : h->stream, h->ev_rel, h->ev_pan, n, H, ldh, h->dinfo, h->pws);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;
@@ -842,7 +850,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
   if (!pr->use_backup) {
     ipm_handle* h = pr->h;
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    potrf_lower_la(st, h->side ? h->side : st, h->ev_rel, h->ev_pan, pr->N, pr->H, pr->ldh, pr->info);
+    potrf_lower_la(st, h->side ? h->side : st, h->ev_rel, h->ev_pan, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     if (h->timing) hipEventRecord(h->ev[3], st);
     potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
   } else {
@@ -873,7 +881,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     const int64_t lds = p + (p & 1);
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, nullptr, 0, pr->tmpn, 0.0, pr->Sbuf, lds, e);
-    potrf_lower(st, p, pr->Sbuf, lds, pr->info);
+    potrf_lower(st, p, pr->Sbuf, lds, pr->info, pr->pws);
     // r = b2 - A (Hi * g)
     mul(st, n, pr->tmpn, pr->g, 1.0, pr->hxs);
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->hxs, 0.0, pr->r2);
@@ -890,7 +898,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   const int64_t lds = p + (p & 1);
   if (!pr->use_backup) {
     potrf_lower_la(st, pr->h->side ? pr->h->side : st, pr->h->ev_rel, pr->h->ev_pan, pr->N, pr->H, pr->ldh,
-                   pr->info);
+                   pr->info, pr->pws);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
     potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
@@ -899,7 +907,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     // S = A Y (lower)
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
-    potrf_lower(st, p, pr->Sbuf, lds, pr->info + 1);
+    potrf_lower(st, p, pr->Sbuf, lds, pr->info + 1, pr->pws);
     // w = S^-1 (b2 - A hg)
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
     lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);

@@ -1,0 +1,223 @@
+// fp64 MFMA tile GEMM for gfx950 (v_mfma_f64_16x16x4_f64): the KKT SYRK of the barrier
+// Hessian and every GEMM-shaped update of the Cholesky factorisation.
+//
+//   C(i, j) (op)= sum_k  w[k] X[k][i] Y[k][j]      i < ni, j < nj, k < K
+//
+// Operands are "k-major": row k of X is X + k*ldx.  That covers both callers without copies:
+//   * KKT assembly (FunctionManager.py:301-306, 801-805): X = Y = C (m x n row-major, k = the
+//     inequality row), w = 1/(s+eps)^2;
+//   * Cholesky updates: a column-major panel A(r, c) at c*lda + r is k-major with k = c.
+// C is column-major (element (i, j) at j*ldc + i), i.e. the lower triangle of the row-major
+// Hessian the reference builds.
+//
+// Workgroup = 256 threads = 2 x 2 waves, 128 x 128 output tile, each wave 64 x 64 = 4 x 4 MFMA
+// tiles (64 fp64 accumulators per lane).  K is staged 16 rows at a time through two LDS
+// buffers (73.7 KB -> 2 workgroups per CU) with the global loads for slab s+2 in registers
+// while slab s is multiplied.  LDS rows are padded to 144 doubles: the 4 k-rows one
+// ds_read_b64 touches sit 32 banks apart (conflict-free).  Full tiles run an unguarded
+// load path; edge tiles (and a ragged last K slab) a guarded one -- a uniform branch.
+// Triangular grids map blockIdx -> tile so that each XCD (blocks b, b+8, ...) sweeps a
+// contiguous run of tile rows and keeps the shared operand panels in its own L2.
+//
+// Measured (tools/gemm_lab.hip, MI355X): 57 TF/s lower-triangle n=8192 K=2048, 50 TF/s at K=256.
+#pragma once
+#include "ipm_common.h"
+
+namespace ipm {
+
+struct GemmArgs {
+  int64_t ni = 0, nj = 0, K = 0;
+  const double* X = nullptr;
+  int64_t ldx = 0;
+  const double* Y = nullptr;
+  int64_t ldy = 0;
+  const double* w = nullptr;     // weight on k (applied to the X operand), may be null
+  double* C = nullptr;
+  int64_t ldc = 0;
+  double alpha = 1.0, beta = 0.0;
+  const double* P = nullptr;     // + tP * P[j*ldp + i]   (row-major symmetric P)
+  int64_t ldp = 0;
+  double tP = 0.0;
+  const double* dvec = nullptr;  // + dvec[i] on the diagonal
+  const int* info = nullptr;     // skip the launch's work when *info != 0 (failed Cholesky)
+  int tri = 0;                   // lower-triangular tile grid (ni == nj), only i >= j written
+  int sub = 0;                   // C -= acc  (alpha/beta/P/dvec ignored)
+  int xcd_remap = 1;             // XCD-contiguous tile order (0: plain blockIdx order)
+  int64_t tiles_i = 0, nblk = 0;
+};
+
+// BM = 128 (4 x 4 MFMA tiles per wave) for large grids, 64 (2 x 2) when the 128-tile grid
+// would leave CUs idle.
+template <int BM_>
+struct MfCfg {
+  static constexpr int BM = BM_, BK = 16, NT = 256;
+  static constexpr int LD = BM + 16;        // padded LDS row: 2*LD == 32 (mod 64) dwords
+  static constexpr int PT = BK * BM / NT;   // doubles per thread per slab per operand
+  static constexpr int TPR = BM / PT;       // threads per slab row
+  static constexpr int TW = BM / 32;        // MFMA tiles per wave per dimension
+};
+
+template <int BM_, bool WEIGHT, bool VEC>
+__global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
+  using M = MfCfg<BM_>;
+  constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TW = M::TW;
+  if (a.info && *a.info != 0) return;
+  __shared__ double sX[2][BK * LD];
+  __shared__ double sY[2][BK * LD];
+  // ---- tile of this workgroup
+  int64_t bi, bj;
+  {
+    int64_t L = blockIdx.x;
+    const int64_t q = a.nblk >> 3;
+    if (a.xcd_remap && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
+    if (a.tri) {
+      int64_t b = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+      while ((b + 1) * (b + 2) / 2 <= L) ++b;
+      while (b * (b + 1) / 2 > L) --b;
+      bi = b;
+      bj = L - b * (b + 1) / 2;
+    } else {
+      bi = L % a.tiles_i;
+      bj = L / a.tiles_i;
+    }
+  }
+  const int64_t I0 = bi * BM, J0 = bj * BM;
+  const bool full = (I0 + BM <= a.ni) && (J0 + BM <= a.nj);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv & 1, wj = wv >> 1;
+  const int sr = tid / TPR, sc = (tid % TPR) * PT;
+  const double* xp = a.X + sr * a.ldx + I0 + sc;
+  const double* yp = a.Y + sr * a.ldy + J0 + sc;
+  const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
+  const int64_t nslab = (a.K + BK - 1) / BK;
+  double rx[PT], ry[PT];
+  auto gload = [&](int64_t s) {
+    const int64_t k = s * BK + sr;
+    const double* xs = xp + s * xstep;
+    const double* ys = yp + s * ystep;
+    if (full && (s + 1) * BK <= a.K) {
+      const double wk = WEIGHT ? a.w[k] : 1.0;
+      if (VEC) {
+#pragma unroll
+        for (int q = 0; q < PT / 2; ++q) {
+          const double2 u = reinterpret_cast<const double2*>(xs)[q];
+          const double2 v = reinterpret_cast<const double2*>(ys)[q];
+          rx[2 * q] = WEIGHT ? u.x * wk : u.x;
+          rx[2 * q + 1] = WEIGHT ? u.y * wk : u.y;
+          ry[2 * q] = v.x;
+          ry[2 * q + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < PT; ++q) {
+          rx[q] = WEIGHT ? xs[q] * wk : xs[q];
+          ry[q] = ys[q];
+        }
+      }
+    } else {
+      const bool kin = k < a.K;
+      const double wk = (WEIGHT && kin) ? a.w[k] : 1.0;
+#pragma unroll
+      for (int q = 0; q < PT; ++q) {
+        const bool xi = kin && (I0 + sc + q < a.ni), yj = kin && (J0 + sc + q < a.nj);
+        rx[q] = xi ? (WEIGHT ? xs[q] * wk : xs[q]) : 0.0;
+        ry[q] = yj ? ys[q] : 0.0;
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      sX[buf][sr * LD + sc + q] = rx[q];
+      sY[buf][sr * LD + sc + q] = ry[q];
+    }
+  };
+  dbl4 acc[TW][TW];
+#pragma unroll
+  for (int u = 0; u < TW; ++u)
+#pragma unroll
+    for (int v = 0; v < TW; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
+  if (nslab > 0) {
+    gload(0);
+    sstore(0);
+    if (nslab > 1) gload(1);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int64_t s = 0; s < nslab; ++s) {
+    const int buf = (int)(s & 1);
+    const double* bx = sX[buf];
+    const double* by = sY[buf];
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double av[TW], bv[TW];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        av[t] = by[(kk * 4 + fk) * LD + wj * (BM / 2) + t * 16 + fr];
+        bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
+      }
+#pragma unroll
+      for (int tj = 0; tj < TW; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TW; ++ti)
+          acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+    }
+    if (s + 1 < nslab) {
+      sstore(buf ^ 1);
+      if (s + 2 < nslab) gload(s + 2);
+    }
+    __syncthreads();
+  }
+  // ---- epilogue: lane holds D[j = fk + 4r][i = fr] of each 16 x 16 tile (f64 MFMA map,
+  //      cdna_hip_programming.md §3) -> 16 consecutive lanes store 16 consecutive i
+#pragma unroll
+  for (int tj = 0; tj < TW; ++tj)
+#pragma unroll
+    for (int ti = 0; ti < TW; ++ti) {
+      const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t j = J0 + wj * (BM / 2) + tj * 16 + fk + 4 * r;
+        if (i < a.ni && j < a.nj && (!a.tri || i >= j)) {
+          double* cp = a.C + j * a.ldc + i;
+          if (a.sub) {
+            *cp -= acc[tj][ti][r];
+          } else {
+            double v = a.alpha * acc[tj][ti][r];
+            if (a.beta != 0.0) v += a.beta * (*cp);
+            if (a.P) v += a.tP * a.P[j * a.ldp + i];
+            if (a.dvec && i == j) v += a.dvec[i];
+            *cp = v;
+          }
+        }
+      }
+    }
+}
+
+template <int BM>
+inline void mfma_gemm_launch_bm(hipStream_t st, GemmArgs a, bool vec) {
+  const int64_t ti = (a.ni + BM - 1) / BM, tj = (a.nj + BM - 1) / BM;
+  a.tiles_i = ti;
+  a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
+  dim3 g((unsigned)a.nblk), b(256);
+  if (a.w) {
+    if (vec) hipLaunchKernelGGL((k_mfma_gemm<BM, true, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_mfma_gemm<BM, true, false>), g, b, 0, st, a);
+  } else {
+    if (vec) hipLaunchKernelGGL((k_mfma_gemm<BM, false, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_mfma_gemm<BM, false, false>), g, b, 0, st, a);
+  }
+}
+
+// launch helper: picks the tile size (grid fill), the weighted / vector-load instantiation
+inline void mfma_gemm_launch(hipStream_t st, GemmArgs a) {
+  if (a.ni <= 0 || a.nj <= 0) return;
+  const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
+                   ((((uintptr_t)a.Y) & 15) == 0);
+  const int64_t ti = (a.ni + 127) / 128, tj = (a.nj + 127) / 128;
+  const int64_t nblk128 = a.tri ? ti * (ti + 1) / 2 : ti * tj;
+  if (nblk128 >= 768) mfma_gemm_launch_bm<128>(st, a, vec);
+  else mfma_gemm_launch_bm<64>(st, a, vec);
+}
+
+}  // namespace ipm

@@ -1,0 +1,28 @@
+// Phase stamps of the Cholesky diagonal-block kernel (diagnostic build; never timed as a result).
+#define IPM_STAMPS 1
+#include "../interiorpoint-gpu_amd/csrc/ipm_blas.hip"
+#include <cstdio>
+#include <vector>
+int main() {
+  const int n = 256, lda = 256;
+  std::vector<double> h((size_t)n * n);
+  srand(3);
+  for (int j = 0; j < n; ++j) for (int i = 0; i < n; ++i) h[(size_t)j * n + i] = (i == j) ? n : (rand() / (double)RAND_MAX - 0.5);
+  for (int j = 0; j < n; ++j) for (int i = 0; i < j; ++i) h[(size_t)j * n + i] = h[(size_t)i * n + j];
+  double *A, *ws; int* info;
+  hipMalloc(&A, h.size() * 8); hipMalloc(&ws, 4096 * 8); hipMalloc(&info, 4);
+  for (int rep = 0; rep < 3; ++rep) {
+    hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice); hipMemset(info, 0, 4);
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(ipm::k_potrf_diag, dim3(1), dim3(512), 0, 0, (int64_t)0, 128, A, (int64_t)lda, ws, info);
+    hipEventRecord(b); hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b);
+    unsigned long long st[64];
+    hipMemcpyFromSymbol(st, HIP_SYMBOL(ipm::ipm_stamps), sizeof(st));
+    printf("rep %d: %.1f us  stamps(cycles from start):", rep, ms * 1e3);
+    for (int i = 1; i < 35; ++i) printf(" %llu", st[i] - st[0]);
+    printf("\n");
+  }
+  return 0;
+}
