@@ -1,0 +1,56 @@
+"""Multi-process host logic of the sharded multi-GPU path (ipm355.dist) on CPU with `gloo`,
+world size 2 and 3: sharding covers every instance exactly once, and the single all_gather
+returns every rank's results to every rank (the solve itself is stubbed -- no GPU here)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from ipm355 import dist as D
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = D.solve_sharded(None, n, solve_fn=lambda i: (1000.0 + i * 0.5, 10 + (i % 7)))
+        np.save(os.path.join(out_dir, f"r{rank}.npy"), res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_partition():
+    for n in (0, 1, 7, 64):
+        for world in (1, 2, 3, 8):
+            got = sorted(i for r in range(world) for i in D.shard(n, r, world))
+            assert got == list(range(n))
+    with pytest.raises(ValueError):
+        D.shard(4, 2, 2)
+
+
+@pytest.mark.parametrize("world,n", [(2, 64), (3, 10)])
+def test_all_gather_results_gloo(tmp_path, world, n):
+    mp.start_processes(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = np.array([[1000.0 + i * 0.5, 10 + (i % 7)] for i in range(n)])
+    for r in range(world):
+        res = np.load(tmp_path / f"r{r}.npy")
+        assert res.shape == (n, 3)
+        np.testing.assert_array_equal(res[:, :2], ref)       # every rank sees every instance
+        assert np.all(res[:, 2] >= 0)
+
+
+def test_single_process_gather_without_init():
+    res = D.gather_results({0: (1.0, 2, 0.1), 2: (3.0, 4, 0.2)}, 3)
+    assert res[0, 0] == 1.0 and res[2, 1] == 4 and np.isnan(res[1, 0])
