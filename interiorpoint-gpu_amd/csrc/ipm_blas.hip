@@ -227,48 +227,88 @@ __device__ unsigned long long ipm_stamps[64];
 #define STAMP() do {} while (0)
 #endif
 
-// LDS footprint 74 KB and <= 128 VGPRs: the kernel fits on a CU beside one trailing-update
-// workgroup (k_mfma_gemm: 73.7 KB, 200 VGPRs), so the look-ahead stream is not starved.
-__global__ __launch_bounds__(512) void k_potrf_diag(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
+// Dinv = L^-1 of a 16 x 16 lower block stored column-major at sblk (element (r,c) at c*16 + r),
+// rinv[r] = 1 / L_rr.  Lane c < 16 computes column c:
+//   X[r][c] = (d_rc - sum_{c<=k<r} L[r][k] X[k][c]) / L_rr ;  written to out (column-major).
+__device__ __forceinline__ void tri_inverse16(const double* sblk, const double* rinv, double* out, int lane) {
+  const int c = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    double v = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < r; ++k) v = fma(-sblk[k * 16 + r], x[k], v);
+    x[r] = (r >= c) ? v * rinv[r] : 0.0;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[c * 16 + r] = x[r];
+  }
+}
+
+// One workgroup, 4 waves.  Chain per 16-column block J: MFMA update of block column J ->
+// wave 0 factors L_JJ in registers -> waves 0-1 solve the tiles below by substitution.  The
+// inverses Dinv_J the TRSM kernel needs are computed by wave 3 while wave 0 factors the NEXT
+// block, i.e. off the chain.
+__global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
                                                     double* __restrict__ dinv_out, int* __restrict__ info) {
-  if (*info != 0) return;
   __shared__ double sD[36 * 256];   // L11 (identity-padded beyond nb)
-  __shared__ double sI[256];        // Dinv_J of the current block column
-  __shared__ double srinv[16];      // 1 / L_cc of the current diagonal block
-  __shared__ double sLr[256];       // L_JJ row-major
+  __shared__ double sLr[256];       // L_JJ row-major (broadcast reads of its rows)
+  __shared__ double srinv[8 * 16];  // 1 / L_cc per diagonal block
+  __shared__ double scol[2][16];    // leaf column broadcast
   __shared__ int fail;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 8 waves
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 4 waves
   const int fr = lane & 15, fk = lane >> 4;
 #ifdef IPM_STAMPS
   int nst = 0;
 #endif
   if (tid == 0) fail = 0;
   STAMP();
-  // ---- load the lower 128 x 128: thread -> rows (2 i2, 2 i2 + 1), columns j = (tid >> 6) + 8q;
-  //      all 16 loads in flight together, branch-free (clamped addresses, selects afterwards)
   const int i0 = 2 * (tid & 63), jb = tid >> 6;
-  {
+  if (nb == PF_NB && ((lda & 1) == 0) && ((k0 & 1) == 0)) {
+    // ---- full panel: the 36 lower blocks go global -> LDS directly (global_load_lds_dwordx4,
+    //      one wave instruction = 8 columns x 16 rows of one block = 1 KB, lane-linear in the
+    //      column-major block image); all 72 in flight at once, 18 per wave.  Upper parts of the
+    //      diagonal blocks arrive as whatever memory holds there: never read (see step 2).
+    int cnt = 0;
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int h = 0; h < 2; ++h, ++cnt)
+          if ((cnt & 3) == wv) {
+            const double* src = A + (k0 + J * 16 + (lane >> 3) + 8 * h) * lda + k0 + I * 16 + 2 * (lane & 7);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)&sD[bidx(I, J) * 256 + h * 128],
+                                             16, 0, 0);
+          }
+    if (*info != 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    // ---- partial panel (last one): register path with identity padding beyond nb
     const bool vec = ((lda & 1) == 0) && ((k0 & 1) == 0);
     const int ic0 = min(i0, nb - 1), ic1 = min(i0 + 1, nb - 1);
     const double* base = A + k0 * lda + k0;
-    double2 v[16];
+    double2 v[32];
     if (vec && i0 + 1 < nb) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int jc = min(jb + 8 * q, nb - 1);
+      for (int q = 0; q < 32; ++q) {
+        const int jc = min(jb + 4 * q, nb - 1);
         v[q] = *reinterpret_cast<const double2*>(base + jc * lda + i0);
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int jc = min(jb + 8 * q, nb - 1);
+      for (int q = 0; q < 32; ++q) {
+        const int jc = min(jb + 4 * q, nb - 1);
         v[q].x = base[jc * lda + ic0];
         v[q].y = base[jc * lda + ic1];
       }
     }
+    if (*info != 0) return;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int j = jb + 8 * q;
+    for (int q = 0; q < 32; ++q) {
+      const int j = jb + 4 * q;
       if ((i0 >> 4) >= (j >> 4)) {
         double2 u;
         u.x = (i0 < j) ? 0.0 : ((i0 < nb && j < nb) ? v[q].x : (i0 == j ? 1.0 : 0.0));
@@ -281,8 +321,10 @@ __global__ __launch_bounds__(512) void k_potrf_diag(int64_t k0, int nb, double* 
   STAMP();
   for (int J = 0; J < 8; ++J) {
     // ---- 1. left-looking update of block column J: T_IJ -= sum_{P<J} L_IP L_JP^T, I >= J
-    if (J > 0 && wv < 8 - J) {
-      const int I = J + wv;
+    //      wave 0 updates the diagonal tile and goes straight on to factor it; waves 1-3 update
+    //      the tiles below meanwhile (no barrier in between)
+    for (int tI = (wv == 0 ? 0 : wv); J > 0 && tI < 8 - J; tI += (wv == 0 ? 8 : 3)) {
+      const int I = J + tI;
       const int cb = bidx(I, J) * 256 + fk * 16 + fr;
       dbl4 acc[4];
 #pragma unroll
@@ -303,74 +345,84 @@ __global__ __launch_bounds__(512) void k_potrf_diag(int64_t k0, int nb, double* 
 #pragma unroll
       for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
     }
-    __syncthreads();
     STAMP();
-    // ---- 2. wave 0: factor the 16 x 16 block (J,J) in registers (lane r = row r), then its
-    //         inverse (lane c = column c of L_JJ^-1, forward substitution with broadcast LDS
-    //         reads of L and the reciprocal pivots)
+    // ---- 2. wave 0: factor the 16 x 16 block (J,J) in registers, lane r = row r.
+    //      Right-looking with NO lane masks: entries above the diagonal (lane r < column c)
+    //      turn into garbage but are never read -- every broadcast reads lane c2 > c or the
+    //      pivot lane.  sqrt and reciprocal come from one rsqrt (off one chain).
     if (wv == 0) {
       const int db = bidx(J, J) * 256;
       const int rr = lane & 15;
       double row[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
-      // Right-looking, NO lane masks: entries above the diagonal (lane r < column c) turn into
-      // garbage but are never read -- every broadcast below reads lane c2 > c or the pivot lane.
+      // Column c+1 is updated first (readlane broadcast) and ITS pivot's rsqrt issued; the rest of
+      // column c's rank-1 update reads column c from an LDS copy (one write, four 32-byte reads
+      // instead of 2 readlanes per element) and fills the rsqrt latency.
+      // Column c+1 is updated first (readlane broadcast) and ITS pivot's rsqrt issued; the rest of
+      // column c's rank-1 update reads column c from an LDS copy (one write, a few wide reads
+      // instead of 2 readlanes per element) and fills the rsqrt latency.
       int bad = 0;
+      double piv = readlane_d(row[0], 0);
+      double dv = rsqrt(piv);
+      double dvs[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        const double piv = readlane_d(row[c], c);
         if (!(piv > 0.0) && bad == 0) bad = c + 1;
-        const double dv = rsqrt(piv);      // 1 / L_cc   (sqrt and reciprocal off one chain)
+        dvs[c] = dv;
         row[c] *= dv;                      // lane c: piv * dv = L_cc
-        if (lane == c) srinv[c] = dv;
+        scol[c & 1][rr] = row[c];          // lanes 16-63 duplicate rows: same value, same address
+        double pivn = 1.0, dvn = 1.0;
+        if (c + 1 < 16) {
+          row[c + 1] = fma(-row[c], readlane_d(row[c], c + 1), row[c + 1]);
+          pivn = readlane_d(row[c + 1], c + 1);
+          dvn = rsqrt(pivn);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) row[c2] = fma(-row[c], readlane_d(row[c], c2), row[c2]);
+        for (int c2 = c + 2; c2 < 16; ++c2) row[c2] = fma(-row[c], scol[c & 1][c2], row[c2]);
+        piv = pivn;
+        dv = dvn;
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (lane == c) srinv[J * 16 + c] = dvs[c];
       }
       if (lane < 16) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           const double v = (rr >= c) ? row[c] : 0.0;
           sD[db + c * 16 + rr] = v;          // column-major block
-          sLr[rr * 16 + c] = v;              // row-major copy for the broadcast reads below
+          sLr[rr * 16 + c] = v;              // row-major copy
         }
       }
       if (lane == 0 && bad) fail = J * 16 + bad;
-      STAMP();
-      // inverse X = L^-1: lane c computes column c, X[r][c] = (d_rc - sum_{k<r} L[r][k] X[k][c]) / L_rr
-      const int c = lane & 15;
-      double x[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        double v = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < r; ++k) v = fma(-sLr[r * 16 + k], x[k], v);
-        x[r] = (r >= c) ? v * srinv[r] : 0.0;
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          sI[c * 16 + r] = x[r];
-          dinv_out[J * 256 + c * 16 + r] = x[r];
-        }
-      }
+    } else if (wv == 3 && J > 0) {
+      // meanwhile (off the chain) wave 3 inverts the PREVIOUS diagonal block for the TRSM kernel
+      tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane);
     }
     __syncthreads();
     STAMP();
     if (fail) break;
-    // ---- 3. L_IJ = T_IJ Dinv_J^T for I > J:  D[j][i] = sum_k Dinv[j][k] T[i][k]
-    if (wv < 7 - J) {
-      const int I = J + 1 + wv;
-      const int cb = bidx(I, J) * 256 + fk * 16 + fr;
-      const int ib = fk * 16 + fr;
-      double bv[4];
+    // ---- 3. tiles below: X = T L_JJ^-T by substitution, one thread per tile row:
+    //      X[r][c] = (T[r][c] - sum_{k<c} X[r][k] L[c][k]) / L_cc
+    if (tid < (7 - J) * 16) {
+      const int I = J + 1 + (tid >> 4), r = tid & 15;
+      const int cb = bidx(I, J) * 256 + r;
+      double x[16];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) bv[s4] = sD[cb + 64 * s4];
-      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+      for (int c = 0; c < 16; ++c) x[c] = sD[cb + c * 16];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sI[ib + 64 * s4], bv[s4], acc, 0, 0, 0);
+      for (int c = 0; c < 16; ++c) {
+        double v = x[c];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = acc[r];
+        for (int k = 0; k < c; ++k) v = fma(-x[k], sLr[c * 16 + k], v);
+        x[c] = v * srinv[J * 16 + c];
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) sD[cb + c * 16] = x[c];
     }
     __syncthreads();
     STAMP();
@@ -379,12 +431,13 @@ __global__ __launch_bounds__(512) void k_potrf_diag(int64_t k0, int nb, double* 
     if (tid == 0) atomicCAS(info, 0, (int)(k0 + fail));
     return;
   }
+  if (wv == 3) tri_inverse16(&sD[bidx(7, 7) * 256], &srinv[7 * 16], dinv_out + 7 * 256, lane);
   // ---- write back L11 (lower part, i < nb, j < nb)
   {
     double* col = A + k0 * lda + k0 + i0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int j = jb + 8 * q;
+    for (int q = 0; q < 32; ++q) {
+      const int j = jb + 4 * q;
       if ((i0 >> 4) >= (j >> 4) && j < nb) {
         const double2 v = *reinterpret_cast<const double2*>(&sD[bidx(i0 >> 4, j >> 4) * 256 + (j & 15) * 16 + (i0 & 15)]);
         if (i0 >= j && i0 < nb) col[j * lda] = v.x;
@@ -468,7 +521,7 @@ __global__ __launch_bounds__(256) void k_potrf_trsm(int64_t n, int64_t k0, int n
 // one panel of width nb <= 128 at column k0: diagonal block, then the rows below it
 static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info,
                          double* ws) {
-  hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(512), 0, st, k0, nb, A, lda, ws, info);
+  hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, st, k0, nb, A, lda, ws, info);
   const int64_t below = n - k0 - nb;
   if (below > 0)
     hipLaunchKernelGGL(k_potrf_trsm, dim3(cdiv(below, PF_RB)), dim3(256), 0, st, n, k0, nb, A, lda,
@@ -480,10 +533,14 @@ static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* 
 //   main stream: update block k+1's columns first, release it to the side stream, then the
 //                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
 // Without a side stream (side == main) the same sequence runs in order.
-void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
-                    double* A, int64_t lda, int* info, double* ws) {
-  hipMemsetAsync(info, 0, sizeof(int), st);
-  const bool two = side != st;
+void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
+                    double* ws) {
+  hipMemsetAsync(info, 0, sizeof(int), caller);
+  const bool two = pst && pst->side;
+  hipStream_t st = (two && pst->main) ? pst->main : caller;
+  hipStream_t side = two ? pst->side : caller;
+  hipEvent_t ev_rel = two ? pst->ev_rel : nullptr, ev_pan = two ? pst->ev_pan : nullptr;
+  if (st != caller) { hipEventRecord(pst->ev_in, caller); hipStreamWaitEvent(st, pst->ev_in, 0); }
   if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
   hipStream_t ps = two ? side : st;
   for (int64_t k0 = 0; k0 < n; k0 += CH_NB) {
@@ -512,10 +569,11 @@ void potrf_lower_la(hipStream_t st, hipStream_t side, hipEvent_t ev_rel, hipEven
                   A + (r0 + w2) * lda + r0 + w2, lda, e, info);
     }
   }
+  if (st != caller) { hipEventRecord(pst->ev_out, st); hipStreamWaitEvent(caller, pst->ev_out, 0); }
 }
 
 void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
-  potrf_lower_la(st, st, nullptr, nullptr, n, A, lda, info, ws);
+  potrf_lower_la(st, nullptr, n, A, lda, info, ws);
 }
 
 // =====================================================================================

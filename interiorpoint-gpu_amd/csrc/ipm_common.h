@@ -59,10 +59,17 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
 // ws: device workspace of POTRF_WS_DOUBLES doubles (the panel's inverted diagonal blocks)
 constexpr int64_t POTRF_WS_DOUBLES = 8 * 256;
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
-// same with one block of look-ahead: panels on `side` (high priority), trailing updates on `s`;
-// ev_rel / ev_pan: two events owned by the caller (re-recorded every block)
-void potrf_lower_la(hipStream_t s, hipStream_t side, hipEvent_t ev_rel, hipEvent_t ev_pan, int64_t n,
-                    double* H, int64_t ldh, int* info_dev, double* ws);
+// same with one block of look-ahead: panels on ps->side (high priority), trailing updates on
+// ps->main; both may be restricted to disjoint CU sets so the panel chain never waits for
+// trailing-update workgroups to drain.  ps == null or ps->side == null: everything in order on
+// `s`.  ps->main == null: trailing updates on `s` itself.  The call is ordered after earlier
+// work on `s`, and later work on `s` is ordered after it.
+struct PotrfStreams {
+  hipStream_t main = nullptr, side = nullptr;
+  hipEvent_t ev_rel = nullptr, ev_pan = nullptr, ev_in = nullptr, ev_out = nullptr;
+};
+void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H, int64_t ldh, int* info_dev,
+                    double* ws);
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,

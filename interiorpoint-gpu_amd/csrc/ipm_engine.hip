@@ -55,8 +55,7 @@ enum Slot {
 struct ipm_handle {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;        // high-priority stream for Cholesky panels (look-ahead)
-  hipEvent_t ev_rel = nullptr, ev_pan = nullptr;
+  PotrfStreams pst;                  // Cholesky look-ahead: panel / trailing streams (CU-masked)
   bool own_stream = false;
   std::string err;
   double* hbuf = nullptr;  // pinned host staging
@@ -430,11 +429,19 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   {
     int least = 0, greatest = 0;
     hipDeviceGetStreamPriorityRange(&least, &greatest);
-    const char* nola = getenv("IPM_NO_LOOKAHEAD");   // debug: run the Cholesky on one stream
-    if (nola && nola[0] == '1') h->side = nullptr;
-    else if (hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, greatest) != hipSuccess) h->side = nullptr;
-    hipEventCreateWithFlags(&h->ev_rel, hipEventDisableTiming);
-    hipEventCreateWithFlags(&h->ev_pan, hipEventDisableTiming);
+    // IPM_NO_LOOKAHEAD=1: Cholesky on the caller's stream only (debug).  Otherwise panels run on
+    // a high-priority side stream, trailing updates on the caller's stream.  (CU-masked streams
+    // were tried: hipExtStreamCreateWithCUMask is not honoured on this platform -- a probe
+    // kernel on a 32-CU-masked stream still ran on all 256 CUs.)
+    const char* nola = getenv("IPM_NO_LOOKAHEAD");
+    PotrfStreams& ps = h->pst;
+    if (!(nola && nola[0] == '1') &&
+        hipStreamCreateWithPriority(&ps.side, hipStreamNonBlocking, greatest) != hipSuccess)
+      ps.side = nullptr;
+    hipEventCreateWithFlags(&ps.ev_rel, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ps.ev_pan, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ps.ev_in, hipEventDisableTiming);
+    hipEventCreateWithFlags(&ps.ev_out, hipEventDisableTiming);
   }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
@@ -453,9 +460,10 @@ extern "C" int ipm_destroy(ipm_handle* h) {
   if (h->pws) hipFree(h->pws);
   if (h->scratch) hipFree(h->scratch);
   for (auto& ev : h->ev) hipEventDestroy(ev);
-  if (h->ev_rel) hipEventDestroy(h->ev_rel);
-  if (h->ev_pan) hipEventDestroy(h->ev_pan);
-  if (h->side) hipStreamDestroy(h->side);
+  for (hipEvent_t e : {h->pst.ev_rel, h->pst.ev_pan, h->pst.ev_in, h->pst.ev_out})
+    if (e) hipEventDestroy(e);
+  if (h->pst.side) hipStreamDestroy(h->pst.side);
+  if (h->pst.main) hipStreamDestroy(h->pst.main);
   if (h->own_stream) hipStreamDestroy(h->stream);
   delete h;
   return IPM_OK;
@@ -501,7 +509,7 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
 
 extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info) {
   if (!h || n < 0 || ldh < n) return IPM_INVALID_ARG;
-  potrf_lower_la(h->stream, h->side ? h->side : h->stream, h->ev_rel, h->ev_pan, n, H, ldh, h->dinfo, h->pws);
+  potrf_lower_la(h->stream, &h->pst, n, H, ldh, h->dinfo, h->pws);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;
@@ -850,7 +858,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
   if (!pr->use_backup) {
     ipm_handle* h = pr->h;
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    potrf_lower_la(st, h->side ? h->side : st, h->ev_rel, h->ev_pan, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
+    potrf_lower_la(st, &h->pst, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     if (h->timing) hipEventRecord(h->ev[3], st);
     potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
   } else {
@@ -897,8 +905,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
   const int64_t lds = p + (p & 1);
   if (!pr->use_backup) {
-    potrf_lower_la(st, pr->h->side ? pr->h->side : st, pr->h->ev_rel, pr->h->ev_pan, pr->N, pr->H, pr->ldh,
-                   pr->info, pr->pws);
+    potrf_lower_la(st, &pr->h->pst, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
     potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);

@@ -15,13 +15,13 @@ int main() {
     hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice); hipMemset(info, 0, 4);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     hipEventRecord(a);
-    hipLaunchKernelGGL(ipm::k_potrf_diag, dim3(1), dim3(512), 0, 0, (int64_t)0, 128, A, (int64_t)lda, ws, info);
+    hipLaunchKernelGGL(ipm::k_potrf_diag, dim3(1), dim3(256), 0, 0, (int64_t)0, 128, A, (int64_t)lda, ws, info);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
     unsigned long long st[64];
     hipMemcpyFromSymbol(st, HIP_SYMBOL(ipm::ipm_stamps), sizeof(st));
     printf("rep %d: %.1f us  stamps(cycles from start):", rep, ms * 1e3);
-    for (int i = 1; i < 35; ++i) printf(" %llu", st[i] - st[0]);
+    for (int i = 1; i < 27; ++i) printf(" %llu", st[i] - st[0]);
     printf("\n");
   }
   return 0;
