@@ -33,6 +33,18 @@ import numpy as np  # noqa: E402
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (256 CU x 2.4 GHz x 128)
 HBM_PEAK_GBS = 8000.0
+# HBM bytes per KKT-SYRK launch from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate
+# passes, FETCH doubled per MI355X_MICROARCH.md) of this same bench: scripts/pmc_summary.py
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_kkt_syrk.json")
+
+
+def pmc_traffic(n, m):
+    """PMC-measured HBM bytes per KKT-SYRK launch, only if the committed profile is of this (n, m)."""
+    try:
+        d = json.load(open(PMC_FILE))
+        return float(d["hbm_bytes_per_launch"]) if (d.get("n"), d.get("m")) == (n, m) else None
+    except Exception:
+        return None
 
 
 def make_instance(n, m, seed, dev):
@@ -86,6 +98,9 @@ def main():
     ap.add_argument("--m", type=int, default=int(os.environ.get("IPM_BENCH_M", 2048)))
     ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("IPM_BENCH_CPU_S", 15)))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--instances", type=int, default=1,
+                    help="independent instances per GPU (config 4: --n 2048 --m 512 --instances 8); each runs "
+                         "`steps` Newton iterations")
     args = ap.parse_args()
 
     import torch
@@ -104,32 +119,35 @@ def main():
     from ipm355 import problems
 
     kwargs = dict(problems.QP_KWARGS)
-    inst = make_instance(args.n, args.m, seed=rank, dev=dev)
+    # one instance: seed = rank (headline); several: seeds 1000 + rank * instances + i
+    seeds = [rank] if args.instances == 1 else [1000 + rank * args.instances + i for i in range(args.instances)]
+    insts = [make_instance(args.n, args.m, seed=sd, dev=dev) for sd in seeds]
 
-    def new_solver():
+    def new_solver(inst):
         return ipm355.QPSolver(check_cvxpy=False, suppress_print=True, device=local, **inst, **kwargs)
 
     # warmup: W iterations on a throw-away solver (kernels, allocator, caches)
     if args.warmup > 0:
-        new_solver().solve(iteration_budget=args.warmup)
-    solver = new_solver()
+        new_solver(insts[0]).solve(iteration_budget=args.warmup)
+    solvers = [new_solver(inst) for inst in insts]      # inputs resident in HBM before timing
     h = L.Handle.get(local)
     h.lib.ipm_set_timing(h.ptr, 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    solver.solve(iteration_budget=args.steps)
+    for solver in solvers:
+        solver.solve(iteration_budget=args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kkt_ms, potrf_ms, cnt = (np.zeros(1) for _ in range(3))
     import ctypes
     a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     h.lib.ipm_last_timings(h.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
     kkt_ms, potrf_ms, cnt = a.value, b.value, c.value
-    done = sum(solver.phase1_solver.inner_iters) + sum(solver.inner_iters)
+    done = sum(sum(s.phase1_solver.inner_iters) + sum(s.inner_iters) for s in solvers)
+    inst = insts[0]
 
     stats = torch.tensor([el, float(done), kkt_ms, potrf_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -155,12 +173,14 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded M3-QP generator, testSolver.py:499-582 shapes)",
             "config": {"workload": f"QPSolver.solve() dense QP n={n}, m={m} ineq, box +-3, phase 1 incl., "
-                                   f"test_QP kwargs; one instance per GPU (seed=rank)",
-                       "n": n, "m": m, "instances_per_gpu": 1, "parallelism": f"instances{world}"},
+                                   f"test_QP kwargs; {args.instances} independent instance(s) per GPU",
+                       "n": n, "m": m, "instances_per_gpu": args.instances,
+                       "parallelism": f"instances{world * args.instances}"},
             "roofline": {"bound": "mfma", "achieved": kkt_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "k_syrk_lower (KKT assembly H = tP + C^T diag(w) C + diag)",
-                         "flops_per_launch": syrk_flops, "avg_launch_ms": float(allst[0, 2])},
+                         "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(n, m),
+                         "kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = tP + C^T diag(w) C + diag)",
+                         "flops_per_launch": syrk_flops, "avg_launch_ms": float(allst[0, 2]),
+                         "algorithmic_bytes_per_launch": 8 * (m * n + m + n * (n + 1) / 2 * 2)},
             "potrf": {"achieved_tflops": potrf_tf, "avg_ms": float(allst[0, 3]), "flops": potrf_flops},
             "whole_iteration_fp64_frac": (f_iter * total_iters / world / tmax) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "newton_iters": total_iters,
