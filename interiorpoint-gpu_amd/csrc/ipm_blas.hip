@@ -209,7 +209,19 @@ void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* 
 constexpr int PF_NB = 128;   // panel width
 constexpr int PF_RB = 64;    // rows per TRSM workgroup
 constexpr int CH_NB = 256;   // outer block (trailing-update depth)
-constexpr int PF_WS = 8 * 256;   // doubles of workspace: the eight Dinv blocks
+constexpr int PF_DINV = 8 * 256;  // workspace doubles: the eight Dinv blocks, then the packed L11 (36 blocks)
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_ctl(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // packed lower 16x16-block storage: block (I,J), I >= J, at bidx(I,J)*256, element (r,c) at c*16+r
 __device__ __forceinline__ int bidx(int I, int J) { return (I * (I + 1)) / 2 + J; }
@@ -227,10 +239,21 @@ __device__ unsigned long long ipm_stamps[64];
 #define STAMP() do {} while (0)
 #endif
 
+// 1/sqrt(x) for the Cholesky pivots (x > 0, normal): v_rsq_f64 plus one third-order correction
+//   e = 1 - x y0^2,  y = y0 + y0 e (1/2 + 3/8 e)
+// (the OCML sequence without its special-value selects, which only matter for x <= 0, inf,
+// denormals: a pivot <= 0 is reported as a failure before its value is used).
+__device__ __forceinline__ double rsqrt_pivot(double x) {
+  const double y0 = __builtin_amdgcn_rsq(x);
+  const double e = fma(-x * y0, y0, 1.0);
+  return fma(y0 * e, fma(e, 0.375, 0.5), y0);
+}
+
 // Dinv = L^-1 of a 16 x 16 lower block stored column-major at sblk (element (r,c) at c*16 + r),
 // rinv[r] = 1 / L_rr.  Lane c < 16 computes column c:
 //   X[r][c] = (d_rc - sum_{c<=k<r} L[r][k] X[k][c]) / L_rr ;  written to out (column-major).
-__device__ __forceinline__ void tri_inverse16(const double* sblk, const double* rinv, double* out, int lane) {
+__device__ __forceinline__ void tri_inverse16(const double* sblk, const double* rinv, double* out, int lane,
+                                              bool sc1) {
   const int c = lane & 15;
   double x[16];
 #pragma unroll
@@ -242,7 +265,10 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
   }
   if (lane < 16) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) out[c * 16 + r] = x[r];
+    for (int r = 0; r < 16; ++r) {
+      if (sc1) st_sc1(&out[c * 16 + r], x[r]);
+      else out[c * 16 + r] = x[r];
+    }
   }
 }
 
@@ -250,13 +276,25 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
 // wave 0 factors L_JJ in registers -> waves 0-1 solve the tiles below by substitution.  The
 // inverses Dinv_J the TRSM kernel needs are computed by wave 3 while wave 0 factors the NEXT
 // block, i.e. off the chain.
-__global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
-                                                    double* __restrict__ dinv_out, int* __restrict__ info) {
-  __shared__ double sD[36 * 256];   // L11 (identity-padded beyond nb)
-  __shared__ double sLr[256];       // L_JJ row-major (broadcast reads of its rows)
-  __shared__ double srinv[8 * 16];  // 1 / L_cc per diagonal block
-  __shared__ double scol[2][16];    // leaf column broadcast
-  __shared__ int fail;
+// Diagonal-block role.  pubL != null: the fused panel kernel's producer -- every final 16 x 16
+// block of L11 is also stored to pubL (packed, sc1) and Dinv_J to dinv_out (sc1); after the
+// barrier that follows each block row's completion, thread 0 raises *progress (sc1).
+struct DiagSmem {
+  double sD[36 * 256];   // L11 (identity-padded beyond nb)
+  double sLr[256];       // L_JJ row-major (broadcast reads of its rows)
+  double srinv[8 * 16];  // 1 / L_cc per diagonal block
+  double scol[2][16];    // leaf column broadcast
+  int fail;
+};
+
+__device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
+                                          double* __restrict__ dinv_out, int* __restrict__ info,
+                                          double* pubL, unsigned* progress, DiagSmem& sm) {
+  double* sD = sm.sD;
+  double* sLr = sm.sLr;
+  double* srinv = sm.srinv;
+  auto& scol = sm.scol;
+  int& fail = sm.fail;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 4 waves
   const int fr = lane & 15, fk = lane >> 4;
 #ifdef IPM_STAMPS
@@ -364,7 +402,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* 
       // instead of 2 readlanes per element) and fills the rsqrt latency.
       int bad = 0;
       double piv = readlane_d(row[0], 0);
-      double dv = rsqrt(piv);
+      double dv = rsqrt_pivot(piv);
       double dvs[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -376,7 +414,7 @@ __global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* 
         if (c + 1 < 16) {
           row[c + 1] = fma(-row[c], readlane_d(row[c], c + 1), row[c + 1]);
           pivn = readlane_d(row[c + 1], c + 1);
-          dvn = rsqrt(pivn);
+          dvn = rsqrt_pivot(pivn);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -400,12 +438,21 @@ __global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* 
       }
       if (lane == 0 && bad) fail = J * 16 + bad;
     } else if (wv == 3 && J > 0) {
-      // meanwhile (off the chain) wave 3 inverts the PREVIOUS diagonal block for the TRSM kernel
-      tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane);
+      // meanwhile (off the chain) wave 3 inverts the PREVIOUS diagonal block for the row part
+      tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
+                    pubL != nullptr);
+    } else if (wv == 2 && J > 0 && pubL) {
+      // ... and wave 2 publishes the previous diagonal block (the chain wave stores nothing)
+      const int db = bidx(J - 1, J - 1) * 256;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
     }
+    if (pubL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     STAMP();
     if (fail) break;
+    // block row J-1 of L11 and Dinv_{J-1} are stored: release them to the row workgroups
+    if (pubL && tid == 0 && J > 0) __hip_atomic_store(progress, (unsigned)J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- 3. tiles below: X = T L_JJ^-T by substitution, one thread per tile row:
     //      X[r][c] = (T[r][c] - sum_{k<c} X[r][k] L[c][k]) / L_cc
     if (tid < (7 - J) * 16) {
@@ -423,15 +470,36 @@ __global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* 
       }
 #pragma unroll
       for (int c = 0; c < 16; ++c) sD[cb + c * 16] = x[c];
+      if (pubL) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) st_sc1(&pubL[cb + c * 16], x[c]);
+      }
     }
     __syncthreads();
     STAMP();
   }
   if (fail) {
-    if (tid == 0) atomicCAS(info, 0, (int)(k0 + fail));
+    if (tid == 0) {
+      atomicCAS(info, 0, (int)(k0 + fail));
+      // release the row workgroups (they finish on garbage; the failed factor is discarded)
+      if (pubL) {
+        __threadfence();
+        __hip_atomic_store(progress, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     return;
   }
-  if (wv == 3) tri_inverse16(&sD[bidx(7, 7) * 256], &srinv[7 * 16], dinv_out + 7 * 256, lane);
+  if (wv == 3) tri_inverse16(&sD[bidx(7, 7) * 256], &srinv[7 * 16], dinv_out + 7 * 256, lane, pubL != nullptr);
+  if (wv == 2 && pubL) {
+    const int db = bidx(7, 7) * 256;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
+  }
+  if (pubL) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(progress, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // ---- write back L11 (lower part, i < nb, j < nb)
   {
     double* col = A + k0 * lda + k0 + i0;
@@ -449,17 +517,19 @@ __global__ __launch_bounds__(256) void k_potrf_diag(int64_t k0, int nb, double* 
 }
 #undef STAMP
 
-__global__ __launch_bounds__(256) void k_potrf_trsm(int64_t n, int64_t k0, int nb, double* __restrict__ A,
-                                                    int64_t lda, const double* __restrict__ dinv,
-                                                    const int* __restrict__ info) {
-  if (*info != 0) return;
-  __shared__ double sL[36 * 256];   // off-diagonal blocks of L11 at bidx (I > J); Dinv_J at bidx(J,J)
+// Row role: rows below the diagonal block, L21 = A21 L11^-T, 64 rows per workgroup, 16 rows per
+// wave.  Each wave runs the 8-step block forward substitution in MFMA registers,
+//   X_J = (B_J - sum_{P<J} X_P L_JP^T) Dinv_J^T,
+// starting step J as soon as the diagonal role has released block row J (*progress > J).
+// L blocks and Dinv come from the producer's sc1 stores and are read with sc1 loads only.
+__device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, int nb, double* __restrict__ A,
+                                         int64_t lda, const double* dinv, const double* pubL,
+                                         unsigned* progress) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
-  const int64_t row0 = k0 + nb + (int64_t)blockIdx.x * PF_RB + wv * 16;
-  const int64_t row = row0 + fr;
+  const int64_t row = k0 + nb + chunk * PF_RB + wv * 16 + fr;
   const bool rin = row < n;
-  // prefetch this wave's 16 x 128 slab of A21 (transposed D layout): acc_J reg r = B[row][J*16 + fk + 4r]
+  // prefetch this wave's 16 x 128 slab of A21 (transposed D layout): b_J reg r = B[row][J*16 + fk + 4r]
   double b[8][4];
 #pragma unroll
   for (int J = 0; J < 8; ++J)
@@ -468,43 +538,31 @@ __global__ __launch_bounds__(256) void k_potrf_trsm(int64_t n, int64_t k0, int n
       const int c = J * 16 + fk + 4 * r;
       b[J][r] = (rin && c < nb) ? A[(k0 + c) * lda + row] : 0.0;
     }
-  // stage L11 (identity-padded like the diagonal kernel) and Dinv
-  {
-    // thread: row i = tid & 127 of columns j = (tid >> 7) + 2q; strictly-lower blocks only; loads in
-    // batches of 16 so they are in flight together
-    const int i = tid & 127;
-    const double* col = A + k0 * lda + k0 + i;
-#pragma unroll
-    for (int qb = 0; qb < 64; qb += 16) {
-      double v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = (tid >> 7) + 2 * (qb + q);
-        v[q] = ((i >> 4) > (j >> 4) && i < nb && j < nb) ? col[j * lda] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int j = (tid >> 7) + 2 * (qb + q);
-        if ((i >> 4) > (j >> 4)) sL[bidx(i >> 4, j >> 4) * 256 + (j & 15) * 16 + (i & 15)] = v[q];
-      }
-    }
-  }
-  for (int idx = tid; idx < 8 * 256; idx += 256) sL[bidx(idx >> 8, idx >> 8) * 256 + (idx & 255)] = dinv[idx];
-  __syncthreads();
   dbl4 x[8];
+  unsigned known = 0;
 #pragma unroll
   for (int J = 0; J < 8; ++J) {
+    while (known <= (unsigned)J) {
+      known = ld_ctl(progress);
+      if (known <= (unsigned)J) __builtin_amdgcn_s_sleep(2);
+    }
     dbl4 acc = dbl4{b[J][0], b[J][1], b[J][2], b[J][3]};
 #pragma unroll
     for (int P = 0; P < J; ++P) {
-      const int ab = bidx(J, P) * 256 + fk * 16 + fr;
+      const double* lb = pubL + bidx(J, P) * 256 + fk * 16 + fr;
+      double av[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-sL[ab + 64 * s4], x[P][s4], acc, 0, 0, 0);
+      for (int s4 = 0; s4 < 4; ++s4) av[s4] = -ld_sc1(lb + 64 * s4);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], x[P][s4], acc, 0, 0, 0);
     }
-    const int ib = bidx(J, J) * 256 + fk * 16 + fr;
+    const double* ib = dinv + J * 256 + fk * 16 + fr;
+    double dvv[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) dvv[s4] = ld_sc1(ib + 64 * s4);
     dbl4 xj = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(sL[ib + 64 * s4], acc[s4], xj, 0, 0, 0);
+    for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(dvv[s4], acc[s4], xj, 0, 0, 0);
     x[J] = xj;
   }
   if (rin) {
@@ -518,14 +576,33 @@ __global__ __launch_bounds__(256) void k_potrf_trsm(int64_t n, int64_t k0, int n
   }
 }
 
-// one panel of width nb <= 128 at column k0: diagonal block, then the rows below it
+// One panel (width nb <= 128 at column k0) in ONE launch.  Workgroups draw tickets: ticket 0 is the
+// diagonal role (so it is resident before anyone waits on it -- no deadlock for any residency),
+// tickets 1.. are the row chunks, pipelined one block column behind the diagonal role.
+// ctl: 2 zeroed words {ticket, progress}.
+__global__ __launch_bounds__(256) void k_potrf_panel(int64_t n, int64_t k0, int nb, double* __restrict__ A,
+                                                     int64_t lda, double* ws, unsigned* ctl, int* __restrict__ info) {
+  __shared__ DiagSmem sm;
+  __shared__ int sticket;
+  if (threadIdx.x == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
+  __syncthreads();
+  const int t = sticket;
+  double* dinv = ws;
+  double* pubL = ws + PF_DINV;
+  if (t == 0) {
+    diag_role(k0, nb, A, lda, dinv, info, pubL, &ctl[1], sm);
+  } else {
+    if (*info != 0) return;
+    row_role(t - 1, n, k0, nb, A, lda, dinv, pubL, &ctl[1]);
+  }
+}
+
+// one panel of width nb <= 128 at column k0 (ctl: this panel's 2 zeroed control words)
 static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info,
-                         double* ws) {
-  hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, st, k0, nb, A, lda, ws, info);
+                         double* ws, unsigned* ctl) {
   const int64_t below = n - k0 - nb;
-  if (below > 0)
-    hipLaunchKernelGGL(k_potrf_trsm, dim3(cdiv(below, PF_RB)), dim3(256), 0, st, n, k0, nb, A, lda,
-                       (const double*)ws, (const int*)info);
+  hipLaunchKernelGGL(k_potrf_panel, dim3(1 + cdiv(std::max<int64_t>(below, 0), PF_RB)), dim3(256), 0, st, n, k0,
+                     nb, A, lda, ws, ctl, info);
 }
 
 // Blocked right-looking Cholesky with one block of look-ahead.
@@ -536,6 +613,8 @@ static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* 
 void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
                     double* ws) {
   hipMemsetAsync(info, 0, sizeof(int), caller);
+  unsigned* ctl = reinterpret_cast<unsigned*>(ws + PF_DINV + 36 * 256);   // 2 words per panel
+  hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned) * cdiv(std::max<int64_t>(n, 1), PF_NB), caller);
   const bool two = pst && pst->side;
   hipStream_t st = (two && pst->main) ? pst->main : caller;
   hipStream_t side = two ? pst->side : caller;
@@ -547,12 +626,12 @@ void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, doub
     const int w = (int)std::min<int64_t>(CH_NB, n - k0);
     // ---- panel k on the side stream
     const int w1 = std::min(w, PF_NB);
-    panel_launch(ps, n, k0, w1, A, lda, info, ws);
+    panel_launch(ps, n, k0, w1, A, lda, info, ws, ctl + 2 * (k0 / PF_NB));
     if (w > w1) {
       // A[k0+w1 : n, k0+w1 : k0+w] -= L[k0+w1 : n, k0 : k0+w1] L[k0+w1 : k0+w, k0 : k0+w1]^T
       gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
                          A + (k0 + w1) * lda + k0 + w1, lda, info);
-      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws);
+      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws, ctl + 2 * ((k0 + w1) / PF_NB));
     }
     if (two) { hipEventRecord(ev_pan, side); hipStreamWaitEvent(st, ev_pan, 0); }
     // ---- trailing update on the main stream
@@ -739,17 +818,6 @@ void trsm_lower_bwd(hipStream_t st, int64_t n, int64_t nrhs, const double* L, in
 // =====================================================================================
 constexpr int TV_B = 64;
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned ld_ctl(unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ double bcast_d(double v, int l) {   // l wave-uniform
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);

@@ -56,8 +56,9 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
                  const double* B, int64_t ldb, double* C, int64_t ldc);
 
 // Cholesky (column-major lower, in place). info_dev: device int (0 or first failing column, 1-based)
-// ws: device workspace of POTRF_WS_DOUBLES doubles (the panel's inverted diagonal blocks)
-constexpr int64_t POTRF_WS_DOUBLES = 8 * 256;
+// ws: device workspace of potrf_ws_doubles(n) doubles (the panel's inverted diagonal blocks,
+// the published L11 blocks, two control words per 128-column panel)
+inline int64_t potrf_ws_doubles(int64_t n) { return 8 * 256 + 36 * 256 + (n + 127) / 128 + 8; }
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
 // same with one block of look-ahead: panels on ps->side (high priority), trailing updates on
 // ps->main; both may be restricted to disjoint CU sets so the panel chain never waits for

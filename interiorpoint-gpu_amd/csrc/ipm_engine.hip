@@ -61,7 +61,8 @@ struct ipm_handle {
   double* hbuf = nullptr;  // pinned host staging
   int* dinfo = nullptr;    // device scratch for level-0 potrf
   unsigned* ctl = nullptr; // device control words for level-0 potrs
-  double* pws = nullptr;   // device workspace for level-0 potrf
+  double* pws = nullptr;   // device workspace for level-0 potrf (grown on demand)
+  int64_t pws_n = 0;
   double* scratch = nullptr;
   size_t scratch_bytes = 0;
   hipEvent_t ev[6];
@@ -183,7 +184,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->mask = c.take<unsigned long long>(4);
   pr->info = c.take<int>(8);
   pr->ctl = c.take<unsigned>(8);
-  pr->pws = c.take<double>(POTRF_WS_DOUBLES);
+  pr->pws = c.take<double>(potrf_ws_doubles(std::max<int64_t>(N, p)));
   pr->coef = c.take<double>(pr->K + 1);
   pr->ones = c.take<double>(pr->K + 1);
   pr->lhs0 = c.take<double>(pr->Lh + 1);
@@ -446,7 +447,6 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   h->ctl = reinterpret_cast<unsigned*>(h->dinfo + 8);
-  if (hipMalloc((void**)&h->pws, POTRF_WS_DOUBLES * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   for (auto& ev : h->ev) hipEventCreate(&ev);
   *out = h;
   return IPM_OK;
@@ -509,6 +509,13 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
 
 extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info) {
   if (!h || n < 0 || ldh < n) return IPM_INVALID_ARG;
+  if (n > h->pws_n) {
+    if (h->pws) hipFree(h->pws);
+    h->pws = nullptr;
+    h->pws_n = 0;
+    HIPCHK(h, hipMalloc((void**)&h->pws, potrf_ws_doubles(n) * sizeof(double)));
+    h->pws_n = n;
+  }
   potrf_lower_la(h->stream, &h->pst, n, H, ldh, h->dinfo, h->pws);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));

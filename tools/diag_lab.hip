@@ -10,12 +10,12 @@ int main() {
   for (int j = 0; j < n; ++j) for (int i = 0; i < n; ++i) h[(size_t)j * n + i] = (i == j) ? n : (rand() / (double)RAND_MAX - 0.5);
   for (int j = 0; j < n; ++j) for (int i = 0; i < j; ++i) h[(size_t)j * n + i] = h[(size_t)i * n + j];
   double *A, *ws; int* info;
-  hipMalloc(&A, h.size() * 8); hipMalloc(&ws, 4096 * 8); hipMalloc(&info, 4);
+  hipMalloc(&A, h.size() * 8); hipMalloc(&ws, 16384 * 8); hipMalloc(&info, 4);
   for (int rep = 0; rep < 3; ++rep) {
     hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice); hipMemset(info, 0, 4);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     hipEventRecord(a);
-    hipLaunchKernelGGL(ipm::k_potrf_diag, dim3(1), dim3(256), 0, 0, (int64_t)0, 128, A, (int64_t)lda, ws, info);
+    hipMemset(ws + 2048 + 9216, 0, 64); hipLaunchKernelGGL(ipm::k_potrf_panel, dim3(1), dim3(256), 0, 0, (int64_t)128, (int64_t)0, 128, A, (int64_t)lda, ws, (unsigned*)(ws + 2048 + 9216), info);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
     unsigned long long st[64];
