@@ -206,9 +206,12 @@ void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* 
 // column-major tile, and the accumulator registers of one product are directly the B
 // operands (k-steps s = r) of the next one -- no shuffles or LDS round trips on the chains.
 // =====================================================================================
+#ifndef IPM_CH_NB
+#define IPM_CH_NB 256
+#endif
 constexpr int PF_NB = 128;   // panel width
 constexpr int PF_RB = 64;    // rows per TRSM workgroup
-constexpr int CH_NB = 256;   // outer block (trailing-update depth)
+constexpr int CH_NB = IPM_CH_NB;   // outer block (trailing-update depth)
 constexpr int PF_DINV = 8 * 256;  // workspace doubles: the eight Dinv blocks, then the packed L11 (36 blocks)
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -416,8 +419,8 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
           pivn = readlane_d(row[c + 1], c + 1);
           dvn = rsqrt_pivot(pivn);
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // (same-wave LDS write -> read: in order, no barrier needed; the compiler keeps the order
+        //  because the addresses may alias)
 #pragma unroll
         for (int c2 = c + 2; c2 < 16; ++c2) row[c2] = fma(-row[c], scol[c & 1][c2], row[c2]);
         piv = pivn;
@@ -605,6 +608,26 @@ static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* 
                      nb, A, lda, ws, ctl, info);
 }
 
+static int num_cus() {
+  static int ncu = -1;
+  if (ncu < 0) {
+    int dev = 0, v = 0;
+    hipGetDevice(&dev);
+    ncu = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return ncu;
+}
+// CUs kept free of trailing-update workgroups while a panel runs (IPM_PANEL_CUS, default 32; 0: off)
+static int panel_reserve_cus() {
+  static int r = -1;
+  if (r < 0) {
+    const char* e = getenv("IPM_PANEL_CUS");
+    r = e ? atoi(e) : 32;
+    if (r < 0 || r >= num_cus()) r = 0;
+  }
+  return r;
+}
+
 // Blocked right-looking Cholesky with one block of look-ahead.
 //   side stream: factor block k (two 128-wide panels + the GEMM between them)
 //   main stream: update block k+1's columns first, release it to the side stream, then the
@@ -643,9 +666,22 @@ void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, doub
                        info);
     if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
     if (n - r0 - w2 > 0) {
-      SyrkEpi e;
-      syrk_launch(st, n - r0 - w2, w, -1.0, A + k0 * lda + r0 + w2, lda, nullptr, 0, nullptr, 1.0,
-                  A + (r0 + w2) * lda + r0 + w2, lda, e, info);
+      GemmArgs a;
+      a.ni = a.nj = n - r0 - w2;
+      a.K = w;
+      a.X = a.Y = A + k0 * lda + r0 + w2;
+      a.ldx = a.ldy = lda;
+      a.C = A + (r0 + w2) * lda + r0 + w2;
+      a.ldc = lda;
+      a.alpha = -1.0;
+      a.beta = 1.0;
+      a.info = info;
+      a.tri = 1;
+      // with the look-ahead running: persistent form on all but panel_reserve_cus() CUs, one
+      // workgroup per CU, so the panel workgroups get CUs of their own (no fp64 MFMA neighbours)
+      const int res = panel_reserve_cus();
+      if (two && res > 0) mfma_gemm_launch_persistent(st, a, num_cus() - res);
+      else mfma_gemm_launch(st, a);
     }
   }
   if (st != caller) { hipEventRecord(pst->ev_out, st); hipStreamWaitEvent(caller, pst->ev_out, 0); }

@@ -21,6 +21,8 @@
 //
 // Measured (tools/gemm_lab.hip, MI355X): 57 TF/s lower-triangle n=8192 K=2048, 50 TF/s at K=256.
 #pragma once
+#include <algorithm>
+
 #include "ipm_common.h"
 
 namespace ipm {
@@ -47,27 +49,34 @@ struct GemmArgs {
 };
 
 // BM = 128 (4 x 4 MFMA tiles per wave) for large grids, 64 (2 x 2) when the 128-tile grid
-// would leave CUs idle.
-template <int BM_>
+// would leave CUs idle.  WJ = waves along j (2: 256 threads, 2 workgroups per CU; 4: 512 threads).
+// PAD > 0 pads the LDS allocation so that only ONE workgroup fits a CU and no Cholesky panel
+// workgroup (77 KB) can share it: the persistent trailing-update form (grid = CUs left to it,
+// each workgroup loops over tiles), which keeps a set of CUs free for the panel stream.
+template <int BM_, int WJ = 2>
 struct MfCfg {
-  static constexpr int BM = BM_, BK = 16, NT = 256;
+  static constexpr int BM = BM_, BK = 16, NT = 128 * WJ;
   static constexpr int LD = BM + 16;        // padded LDS row: 2*LD == 32 (mod 64) dwords
   static constexpr int PT = BK * BM / NT;   // doubles per thread per slab per operand
   static constexpr int TPR = BM / PT;       // threads per slab row
-  static constexpr int TW = BM / 32;        // MFMA tiles per wave per dimension
+  static constexpr int TWI = BM / 32;       // MFMA tiles per wave along i (2 waves)
+  static constexpr int TWJ = BM / (16 * WJ);  // ... along j (WJ waves)
 };
 
-template <int BM_, bool WEIGHT, bool VEC>
-__global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
-  using M = MfCfg<BM_>;
-  constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TW = M::TW;
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
+__global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a) {
+  using M = MfCfg<BM_, WJ>;
+  constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
   if (a.info && *a.info != 0) return;
   __shared__ double sX[2][BK * LD];
   __shared__ double sY[2][BK * LD];
+  __shared__ double spad[PAD > 0 ? PAD : 1];
+  if (PAD > 0 && a.ni < 0) spad[threadIdx.x] = 0.0;   // never executed: keeps the pad allocated
+  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
   // ---- tile of this workgroup
   int64_t bi, bj;
   {
-    int64_t L = blockIdx.x;
+    int64_t L = Lw;
     const int64_t q = a.nblk >> 3;
     if (a.xcd_remap && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
     if (a.tri) {
@@ -90,6 +99,10 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
   const double* yp = a.Y + sr * a.ldy + J0 + sc;
   const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
   const int64_t nslab = (a.K + BK - 1) / BK;
+  // C -= X^T Y (Cholesky updates): the accumulators start FROM the C tile (its loads overlap the
+  // first slab's) and X is staged negated -- no dependent C read in the epilogue
+  const bool cinit = a.sub || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
+  const double xsg = cinit ? -1.0 : 1.0;
   double rx[PT], ry[PT];
   auto gload = [&](int64_t s) {
     const int64_t k = s * BK + sr;
@@ -102,15 +115,15 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
         for (int q = 0; q < PT / 2; ++q) {
           const double2 u = reinterpret_cast<const double2*>(xs)[q];
           const double2 v = reinterpret_cast<const double2*>(ys)[q];
-          rx[2 * q] = WEIGHT ? u.x * wk : u.x;
-          rx[2 * q + 1] = WEIGHT ? u.y * wk : u.y;
+          rx[2 * q] = (WEIGHT ? u.x * wk : u.x) * xsg;
+          rx[2 * q + 1] = (WEIGHT ? u.y * wk : u.y) * xsg;
           ry[2 * q] = v.x;
           ry[2 * q + 1] = v.y;
         }
       } else {
 #pragma unroll
         for (int q = 0; q < PT; ++q) {
-          rx[q] = WEIGHT ? xs[q] * wk : xs[q];
+          rx[q] = (WEIGHT ? xs[q] * wk : xs[q]) * xsg;
           ry[q] = ys[q];
         }
       }
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
         const bool xi = kin && (I0 + sc + q < a.ni), yj = kin && (J0 + sc + q < a.nj);
-        rx[q] = xi ? (WEIGHT ? xs[q] * wk : xs[q]) : 0.0;
+        rx[q] = xi ? (WEIGHT ? xs[q] * wk : xs[q]) * xsg : 0.0;
         ry[q] = yj ? ys[q] : 0.0;
       }
     }
@@ -132,34 +145,46 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
       sY[buf][sr * LD + sc + q] = ry[q];
     }
   };
-  dbl4 acc[TW][TW];
+  const int fr = lane & 15, fk = lane >> 4;
+  dbl4 acc[TWJ][TWI];
 #pragma unroll
-  for (int u = 0; u < TW; ++u)
+  for (int u = 0; u < TWJ; ++u)
 #pragma unroll
-    for (int v = 0; v < TW; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int v = 0; v < TWI; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
+  if (cinit) {
+#pragma unroll
+    for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+      for (int ti = 0; ti < TWI; ++ti) {
+        const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
+          acc[tj][ti][r] = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
+        }
+      }
+  }
   if (nslab > 0) {
     gload(0);
     sstore(0);
     if (nslab > 1) gload(1);
   }
   __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
   for (int64_t s = 0; s < nslab; ++s) {
     const int buf = (int)(s & 1);
     const double* bx = sX[buf];
     const double* by = sY[buf];
 #pragma unroll
     for (int kk = 0; kk < BK / 4; ++kk) {
-      double av[TW], bv[TW];
+      double av[TWJ], bv[TWI];
 #pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        av[t] = by[(kk * 4 + fk) * LD + wj * (BM / 2) + t * 16 + fr];
-        bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
-      }
+      for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
 #pragma unroll
-      for (int tj = 0; tj < TW; ++tj)
+      for (int t = 0; t < TWI; ++t) bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
 #pragma unroll
-        for (int ti = 0; ti < TW; ++ti)
+      for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TWI; ++ti)
           acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
     }
     if (s + 1 < nslab) {
@@ -171,17 +196,17 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
   // ---- epilogue: lane holds D[j = fk + 4r][i = fr] of each 16 x 16 tile (f64 MFMA map,
   //      cdna_hip_programming.md §3) -> 16 consecutive lanes store 16 consecutive i
 #pragma unroll
-  for (int tj = 0; tj < TW; ++tj)
+  for (int tj = 0; tj < TWJ; ++tj)
 #pragma unroll
-    for (int ti = 0; ti < TW; ++ti) {
+    for (int ti = 0; ti < TWI; ++ti) {
       const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t j = J0 + wj * (BM / 2) + tj * 16 + fk + 4 * r;
+        const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
         if (i < a.ni && j < a.nj && (!a.tri || i >= j)) {
           double* cp = a.C + j * a.ldc + i;
-          if (a.sub) {
-            *cp -= acc[tj][ti][r];
+          if (cinit) {
+            *cp = acc[tj][ti][r];
           } else {
             double v = a.alpha * acc[tj][ti][r];
             if (a.beta != 0.0) v += a.beta * (*cp);
@@ -192,6 +217,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm(GemmArgs a) {
         }
       }
     }
+  }   // persistent tile loop
 }
 
 template <int BM>
@@ -207,6 +233,21 @@ inline void mfma_gemm_launch_bm(hipStream_t st, GemmArgs a, bool vec) {
     if (vec) hipLaunchKernelGGL((k_mfma_gemm<BM, false, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_mfma_gemm<BM, false, false>), g, b, 0, st, a);
   }
+}
+
+// persistent one-workgroup-per-CU form (no weight): at most `max_wg` workgroups loop over the
+// 128-tiles; used for the Cholesky trailing update while the panel stream owns the other CUs
+inline void mfma_gemm_launch_persistent(hipStream_t st, GemmArgs a, int max_wg) {
+  if (a.ni <= 0 || a.nj <= 0) return;
+  const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
+                   ((((uintptr_t)a.Y) & 15) == 0);
+  const int64_t ti = (a.ni + 127) / 128, tj = (a.nj + 127) / 128;
+  a.tiles_i = ti;
+  a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
+  dim3 g((unsigned)std::min<int64_t>(a.nblk, max_wg)), b(512);
+  constexpr int PAD = 2200;   // 73.7 + 17.6 KB: one per CU, and no 77 KB panel workgroup beside it
+  if (vec) hipLaunchKernelGGL((k_mfma_gemm<128, false, true, 4, PAD>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((k_mfma_gemm<128, false, false, 4, PAD>), g, b, 0, st, a);
 }
 
 // launch helper: picks the tile size (grid fill), the weighted / vector-load instantiation

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libipm355.so")
+LIB_PATH = os.environ.get("IPM355_LIB", os.path.join(_HERE, "libipm355.so"))   # override: experiments only
 
 IPM_OK = 0
 IPM_NOT_POSITIVE_DEFINITE = 1

@@ -4,7 +4,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows = [r for r in rows if "ipm::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # last potrf = kernels after the last k_potrf_diag with k0 == 0 ... approximate: take the second half
-starts = [i for i, r in enumerate(rows) if "k_potrf_diag" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "k_potrf_diag" in r["Kernel_Name"] or "k_potrf_panel" in r["Kernel_Name"]]
 half = starts[len(starts) // 2]
 rows = rows[half:]
 t0 = int(rows[0]["Start_Timestamp"]); t1 = max(int(r["End_Timestamp"]) for r in rows)

@@ -12,10 +12,10 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
 // BM x BN workgroup tile, WM x WN waves, BK-deep slabs, NSTAGE LDS stages
-template <int BM, int BN, int WM, int WN, int BK, bool TRI>
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int PAD = 0>
 __global__ __launch_bounds__(WM * WN * 64) void k_gemm(int n, int K, const double* __restrict__ X, int ldx,
                                                         const double* __restrict__ Y, int ldy,
-                                                        double* __restrict__ C, int ldc, int tiles_i) {
+                                                        double* __restrict__ C, int ldc, int tiles_i, int nblk) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;   // MFMA tiles per wave
   constexpr int LX = BM + 16, LY = BN + 16;              // padded LDS rows
@@ -23,15 +23,18 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm(int n, int K, const doubl
   static_assert(PX % 2 == 0 && PY % 2 == 0, "pairs");
   __shared__ double sX[2][BK * LX];
   __shared__ double sY[2][BK * LY];
+  __shared__ double spad[PAD > 0 ? PAD : 1];
+  if (PAD > 0 && threadIdx.x == 0 && n < 0) spad[0] = 0.0;   // keep the pad allocated
+  for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
   int bi, bj;
   if (TRI) {
-    const int L = blockIdx.x;
+    const int L = Lp;
     int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
     while ((b + 1) * (b + 2) / 2 <= L) ++b;
     while (b * (b + 1) / 2 > L) --b;
     bi = b; bj = L - b * (b + 1) / 2;   // BM == BN for TRI
   } else {
-    bi = blockIdx.x % tiles_i; bj = blockIdx.x / tiles_i;
+    bi = Lp % tiles_i; bj = Lp / tiles_i;
   }
   const int I0 = bi * BM, J0 = bj * BN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -98,6 +101,8 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm(int n, int K, const doubl
         if (!TRI || i >= j) C[(size_t)j * ldc + i] = acc[tj][ti][r];
       }
     }
+  __syncthreads();
+  }
 }
 
 __global__ void k_ref(int n, int K, const double* X, int ldx, const double* Y, int ldy, double* C, int ldc) {
@@ -108,12 +113,12 @@ __global__ void k_ref(int n, int K, const double* X, int ldx, const double* Y, i
   C[(size_t)j * ldc + i] = s;
 }
 
-template <int BM, int BN, int WM, int WN, int BK, bool TRI>
-void run(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps) {
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int PAD = 0>
+void run(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps, int grid = 0) {
   const int ti = n / BM, tj = n / BN;
   const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
   auto launch = [&]() {
-    hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, BK, TRI>), dim3(nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti);
+    hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, BK, TRI, PAD>), dim3(grid ? grid : nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti, nblk);
   };
   CK(hipMemset(C, 0, (size_t)n * n * 8));
   launch();
@@ -137,24 +142,25 @@ void run(const char* name, int n, int K, double* X, double* Y, double* C, double
 }
 
 void runlib(const char* name, int n, int K, bool tri, bool weight, int remap, double* X, double* C, double* R,
-            double* w, int reps) {
+            double* w, int reps, int persist = 0, double beta = 0.0) {
   ipm::GemmArgs a;
   a.ni = n; a.nj = n; a.K = K; a.X = X; a.ldx = n; a.Y = X; a.ldy = n; a.w = weight ? w : nullptr;
-  a.C = C; a.ldc = n; a.tri = tri; a.xcd_remap = remap;
+  a.C = C; a.ldc = n; a.tri = tri; a.xcd_remap = remap; a.beta = beta; if (beta == 1.0) a.alpha = -1.0;
   CK(hipMemset(C, 0, (size_t)n * n * 8));
-  ipm::mfma_gemm_launch(0, a);
+  auto L = [&]() { if (persist) ipm::mfma_gemm_launch_persistent(0, a, persist); else ipm::mfma_gemm_launch(0, a); };
+  L();
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   float best = 1e30, tot = 0;
   for (int r = 0; r < reps; ++r) {
-    CK(hipEventRecord(e0)); ipm::mfma_gemm_launch(0, a); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    CK(hipEventRecord(e0)); L(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = std::min(best, ms); tot += ms;
   }
   std::vector<double> hc((size_t)n * n), hr((size_t)n * n);
   CK(hipMemcpy(hc.data(), C, (size_t)n * n * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(hr.data(), R, (size_t)n * n * 8, hipMemcpyDeviceToHost));
   double err = 0, mx = 0;
-  if (!weight)
+  if (!weight && beta == 0.0)
     for (int j = 0; j < n; j += 97)
       for (int i = tri ? j : 0; i < n; ++i) { err = std::max(err, fabs(hc[(size_t)j * n + i] - hr[(size_t)j * n + i])); mx = std::max(mx, fabs(hr[(size_t)j * n + i])); }
   const double fl = tri ? (double)n * (n + 1) * K : 2.0 * n * n * K;
@@ -177,18 +183,12 @@ int main(int argc, char** argv) {
   double* w; CK(hipMalloc(&w, (size_t)K * 8));
   { std::vector<double> hw(K, 1.5); CK(hipMemcpy(w, hw.data(), K * 8, hipMemcpyHostToDevice)); }
   runlib("lib tri remap", n, K, true, false, 1, X, C, R, w, reps);
-  runlib("lib tri noremap", n, K, true, false, 0, X, C, R, w, reps);
-  runlib("lib tri weighted remap", n, K, true, true, 1, X, C, R, w, reps);
-  runlib("lib full remap", n, K, false, false, 1, X, C, R, w, reps);
-  runlib("lib full noremap", n, K, false, false, 0, X, C, R, w, reps);
-  run<128, 128, 2, 2, 16, true>("tri 128x128 w2x2 bk16", n, K, X, X, C, R, reps);
-  run<128, 128, 2, 2, 32, true>("tri 128x128 w2x2 bk32", n, K, X, X, C, R, reps);
-  run<128, 128, 2, 4, 16, true>("tri 128x128 w2x4 bk16", n, K, X, X, C, R, reps);
-  // run<256, 256, 2, 4, 16, true>("tri 256x256 w2x4 bk16", n, K, X, X, C, R, reps);
-  run<128, 128, 2, 2, 16, false>("full 128x128 w2x2 bk16", n, K, X, X, C, R, reps);
-  run<256, 128, 4, 2, 16, false>("full 256x128 w4x2 bk16", n, K, X, X, C, R, reps);
-  run<128, 256, 2, 4, 16, false>("full 128x256 w2x4 bk16", n, K, X, X, C, R, reps);
-  run<128, 256, 2, 2, 16, false>("full 128x256 w2x2 bk16", n, K, X, X, C, R, reps);
-  // run<256, 256, 4, 4, 8, false>("full 256x256 w4x4 bk8", n, K, X, X, C, R, reps);
+  runlib("lib tri remap beta1", n, K, true, false, 1, X, C, R, w, reps, 0, 1.0);
+  runlib("lib persist224 remap", n, K, true, false, 1, X, C, R, w, reps, 224);
+  runlib("lib persist224 noremap", n, K, true, false, 0, X, C, R, w, reps, 224);
+  runlib("lib persist224 remap beta1", n, K, true, false, 1, X, C, R, w, reps, 224, 1.0);
+  runlib("lib persist224 noremap beta1", n, K, true, false, 0, X, C, R, w, reps, 224, 1.0);
+  runlib("lib persist256 noremap beta1", n, K, true, false, 0, X, C, R, w, reps, 256, 1.0);
+  run<128, 128, 2, 4, 16, true, 2200>("lab w2x4 pad persist224", n, K, X, X, C, R, reps, 224);
   return 0;
 }
