@@ -863,8 +863,8 @@ __device__ __forceinline__ double bcast_d(double v, int l) {   // l wave-uniform
 // FWD: solve L y = b.   !FWD: solve L^T y = b.   L column-major lower (ldl); y must not alias b.
 template <bool FWD>
 __global__ __launch_bounds__(256) void k_trsv_chain(int64_t n, int nblk, const double* __restrict__ L,
-                                                    int64_t ldl, const double* __restrict__ b, double* y,
-                                                    unsigned* ctl) {
+                                                    int64_t ldl, const double* __restrict__ b, int64_t bstride,
+                                                    double* y, unsigned* ctl) {
   __shared__ double sL[TV_B * (TV_B + 1)];        // diagonal block, column-major, padded
   __shared__ double sdinv[TV_B];
   __shared__ double sacc[TV_B * (TV_B + 1)];      // cross-wave / cross-lane partial sums
@@ -952,7 +952,7 @@ __global__ __launch_bounds__(256) void k_trsv_chain(int64_t n, int nblk, const d
         s = 0.0;
         for (int l = 0; l < TV_B; ++l) s += sacc[lane * (TV_B + 1) + l];
       }
-      double r = lane < rows ? b[r0 + lane] - s : 0.0;
+      double r = lane < rows ? b[(r0 + lane) * bstride] - s : 0.0;
       const double dinv = sdinv[lane];
       // Substitution out of registers.  lv holds the STRICTLY triangular part of the lane's
       // row (fwd) / column (bwd), so step j leaves lanes <= j (fwd) / >= j (bwd) untouched and
@@ -981,13 +981,33 @@ __global__ __launch_bounds__(256) void k_trsv_chain(int64_t n, int nblk, const d
 }
 
 static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int64_t ldl, const double* b,
-                       double* y, unsigned* ctl) {
+                       int64_t bstride, double* y, unsigned* ctl) {
   const int nblk = (int)cdiv(n, TV_B);
   const int grid = std::min(nblk, 1024);
   if (fwd)
-    hipLaunchKernelGGL(k_trsv_chain<true>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, y, ctl);
+    hipLaunchKernelGGL(k_trsv_chain<true>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, bstride, y, ctl);
   else
-    hipLaunchKernelGGL(k_trsv_chain<false>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, y, ctl);
+    hipLaunchKernelGGL(k_trsv_chain<false>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, bstride, y, ctl);
+}
+
+// L^T x = b (b read with stride bstride, e.g. the bordered row of a Cholesky factor); ctl: 2 words
+void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
+                  double* x, unsigned* ctl) {
+  if (n <= 0) return;
+  hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned), st);
+  trsv_chain(st, false, n, L, ldl, b, bstride, x, ctl);
+}
+
+// Bordered right-hand side: row N of the (N+1) x (N+1) column-major lower factor input holds
+// rhs^T and the corner a huge value, so that the Cholesky factor's row N is (L^-1 rhs)^T -- the
+// forward substitution comes out of the factorisation itself (Cholesky of [[H, r], [r^T, c]]).
+__global__ void k_border_rhs(int64_t N, double* H, int64_t ldh, const double* g, double scale, double corner) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < N) H[j * ldh + N] = scale * g[j];
+  else if (j == N) H[N * ldh + N] = corner;
+}
+void border_rhs(hipStream_t st, int64_t N, double* H, int64_t ldh, const double* g, double scale) {
+  hipLaunchKernelGGL(k_border_rhs, dim3(cdiv(N + 1, 256)), dim3(256), 0, st, N, H, ldh, g, scale, 1e300);
 }
 
 // L L^T X = B in place; W: scratch n x nrhs (ldb); ctl: device scratch of 4 words (single
@@ -997,8 +1017,8 @@ void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64
   if (n <= 0 || nrhs <= 0) return;
   if (nrhs == 1 && ldb == 1 && ctl) {
     hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned), st);
-    trsv_chain(st, true, n, L, ldl, B, W, ctl);
-    trsv_chain(st, false, n, L, ldl, W, B, ctl + 2);
+    trsv_chain(st, true, n, L, ldl, B, 1, W, ctl);
+    trsv_chain(st, false, n, L, ldl, W, 1, B, ctl + 2);
     return;
   }
   trsm_lower_fwd(st, n, nrhs, L, ldl, B, ldb, W);

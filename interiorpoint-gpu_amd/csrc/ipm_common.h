@@ -75,6 +75,11 @@ void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H,
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                  int64_t ldb, double* W, unsigned* ctl);
+// L^T x = b, one right-hand side read with stride bstride; ctl: 2 device words
+void trsv_lower_t(hipStream_t s, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
+                  double* x, unsigned* ctl);
+// H[j*ldh + N] = scale * g[j] (j < N), H[N*ldh + N] = 1e300: bordered right-hand side (see ipm_blas.hip)
+void border_rhs(hipStream_t s, int64_t N, double* H, int64_t ldh, const double* g, double scale);
 // forward L Y = B / backward L^T Y = B: B is consumed, the solution goes to Y (same ld)
 void trsm_lower_fwd(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                     int64_t ldb, double* Y);

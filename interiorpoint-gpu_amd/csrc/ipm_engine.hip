@@ -151,7 +151,8 @@ void derive(ipm_problem* pr) {
     pr->S = pr->m + pr->nub + pr->nlb;
     pr->Sbar = pr->S;
   }
-  pr->ldh = pr->N + (pr->N & 1);
+  // room for one bordered row (N+1 rows): the Newton right-hand side rides through the Cholesky
+  pr->ldh = (pr->N + 1) + ((pr->N + 1) & 1);
 }
 
 int64_t carve(ipm_problem* pr, char* base) {
@@ -184,7 +185,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->mask = c.take<unsigned long long>(4);
   pr->info = c.take<int>(8);
   pr->ctl = c.take<unsigned>(8);
-  pr->pws = c.take<double>(potrf_ws_doubles(std::max<int64_t>(N, p)));
+  pr->pws = c.take<double>(potrf_ws_doubles(std::max<int64_t>(N + 1, p)));
   pr->coef = c.take<double>(pr->K + 1);
   pr->ones = c.take<double>(pr->K + 1);
   pr->lhs0 = c.take<double>(pr->Lh + 1);
@@ -198,7 +199,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->nls_blocks = nls;
   pr->pmask = c.take<unsigned long long>(nls + 1);
   pr->psum = c.take<double>((nls + 1) * NCAND);
-  pr->H = c.take<double>(pr->ldh * N);
+  pr->H = c.take<double>(pr->ldh * (N + 1));
   pr->W2 = c.take<double>(N * std::max<int64_t>(p, 1));
   pr->piv = c.take<int64_t>(N);
   if (pr->eq) {
@@ -861,14 +862,17 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     return IPM_OK;
   }
   assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
-  lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
   if (!pr->use_backup) {
+    // Cholesky of the bordered [[H, -g], [-g^T, big]]: its last row is y = L^-1 (-g) (the forward
+    // solve of NewtonSolver.py:287-299 / cho_solve), then one backward solve L^T dx = y
     ipm_handle* h = pr->h;
+    border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    potrf_lower_la(st, &h->pst, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
+    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws);
     if (h->timing) hipEventRecord(h->ev[3], st);
-    potrs_lower(st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
+    trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl);
   } else {
+    lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
     if (rc) return rc;
     getrf(st, pr->N, pr->H, pr->ldh, pr->piv, pr->info);
