@@ -19,6 +19,7 @@ Cholesky rate, and the CPU oracle timed on a bounded sample of the same workload
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -98,10 +99,17 @@ def main():
     ap.add_argument("--m", type=int, default=int(os.environ.get("IPM_BENCH_M", 2048)))
     ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("IPM_BENCH_CPU_S", 15)))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="solve the instances concurrently: one HIP stream + host thread each")
     ap.add_argument("--instances", type=int, default=1,
                     help="independent instances per GPU (config 4: --n 2048 --m 512 --instances 8); each runs "
                          "`steps` Newton iterations")
     args = ap.parse_args()
+    if args.concurrent:
+        # each instance = its stream + its Cholesky panel stream; HIP maps streams onto
+        # GPU_MAX_HW_QUEUES hardware queues (4 by default) -- streams sharing a queue serialise.
+        # Must be set before the HIP runtime starts.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
     import torch
     import torch.distributed as dist
@@ -126,18 +134,39 @@ def main():
     def new_solver(inst):
         return ipm355.QPSolver(check_cvxpy=False, suppress_print=True, device=local, **inst, **kwargs)
 
-    # warmup: W iterations on a throw-away solver (kernels, allocator, caches)
+    # one stream per instance when concurrent (solvers bind their handle to the current stream)
+    streams = [torch.cuda.Stream(device=dev) for _ in insts] if args.concurrent else [None] * len(insts)
+
+    def on(stream):
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    # warmup: W iterations on a throw-away solver per stream (kernels, allocator, caches)
     if args.warmup > 0:
-        new_solver(insts[0]).solve(iteration_budget=args.warmup)
-    solvers = [new_solver(inst) for inst in insts]      # inputs resident in HBM before timing
-    h = L.Handle.get(local)
+        for inst, stm in zip(insts, streams if args.concurrent else streams[:1]):
+            with on(stm):
+                new_solver(inst).solve(iteration_budget=args.warmup)
+    solvers = []
+    for inst, stm in zip(insts, streams):                 # inputs resident in HBM before timing
+        with on(stm):
+            solvers.append(new_solver(inst))
+    with on(streams[0]):
+        h = L.Handle.get(local)
     h.lib.ipm_set_timing(h.ptr, 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for solver in solvers:
-        solver.solve(iteration_budget=args.steps)
+    if args.concurrent:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def run(k):
+            with on(streams[k]):
+                solvers[k].solve(iteration_budget=args.steps)
+        with ThreadPoolExecutor(max_workers=len(solvers)) as ex:
+            list(ex.map(run, range(len(solvers))))
+    else:
+        for solver in solvers:
+            solver.solve(iteration_budget=args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -173,7 +202,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded M3-QP generator, testSolver.py:499-582 shapes)",
             "config": {"workload": f"QPSolver.solve() dense QP n={n}, m={m} ineq, box +-3, phase 1 incl., "
-                                   f"test_QP kwargs; {args.instances} independent instance(s) per GPU",
+                                   f"test_QP kwargs; {args.instances} independent instance(s) per GPU"
+                                   + (" solved concurrently (one stream + host thread each)" if args.concurrent else ""),
                        "n": n, "m": m, "instances_per_gpu": args.instances,
                        "parallelism": f"instances{world * args.instances}"},
             "roofline": {"bound": "mfma", "achieved": kkt_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -108,29 +108,38 @@ def load_library(path: str = LIB_PATH):
 
 
 class Handle:
-    """One ipm_handle per (process, device, stream); wraps torch's current stream."""
+    """One ipm_handle per (process, device, stream): bound to torch's CURRENT stream at creation.
+
+    Solvers built under different `torch.cuda.stream(...)` contexts get different handles, so
+    independent instances can run concurrently from host threads (the C calls release the GIL).
+    """
 
     _cache = {}
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, stream: int = 0):
         import torch
         if not torch.cuda.is_available():
             raise IPMBackendError("no HIP device visible: the ipm355 solvers run on MI355X only")
         self.lib = load_library()
         self.device = device
+        self.stream = stream
         self.torch_device = torch.device("cuda", device)
-        with torch.cuda.device(device):
-            stream = torch.cuda.current_stream(device).cuda_stream
         h = P()
         self.check(self.lib.ipm_create(device, P(stream), C.byref(h)), None)
         self.ptr = h
 
     @classmethod
     def get(cls, device: int = 0) -> "Handle":
-        h = cls._cache.get(device)
+        import torch
+        if not torch.cuda.is_available():
+            raise IPMBackendError("no HIP device visible: the ipm355 solvers run on MI355X only")
+        with torch.cuda.device(device):
+            stream = torch.cuda.current_stream(device).cuda_stream
+        key = (device, stream)
+        h = cls._cache.get(key)
         if h is None:
-            h = cls(device)
-            cls._cache[device] = h
+            h = cls(device, stream)
+            cls._cache[key] = h
         return h
 
     def check(self, rc, h=None):

@@ -126,3 +126,37 @@ def test_group_lasso_fstar_known_answer():
     z, s, v = _run("socp_group_lasso")
     assert abs(v + float(z["yty_over_2n"]) - float(z["fstar"])) < 1e-6
     assert s.phase1_solver.phase1_ns.use_backup
+
+
+def test_concurrent_instances_match_sequential():
+    """Independent instances solved from host threads on their own HIP streams (per-stream
+    handles, the config-4 batch mode) give bit-identical results to solving them one by one."""
+    import threading
+
+    import torch
+
+    import ipm355
+    from ipm355 import problems
+    kws = [dict(problems.qp_ineq_box(256, 64, seed=50 + i), **problems.QP_KWARGS) for i in range(4)]
+    seq = []
+    for kw in kws:
+        s = ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw)
+        s.solve()
+        seq.append(np.array(s.xstar))
+    streams = [torch.cuda.Stream() for _ in kws]
+    solvers = []
+    for kw, st in zip(kws, streams):
+        with torch.cuda.stream(st):
+            solvers.append(ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw))
+
+    def run(k):
+        with torch.cuda.stream(streams[k]):
+            solvers[k].solve()
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(kws))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    for s, ref in zip(solvers, seq):
+        np.testing.assert_array_equal(np.array(s.xstar), ref)
