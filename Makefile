@@ -23,7 +23,17 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 $(OUT): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
+# diagnostic library: per-workgroup role timestamps of one Cholesky launch (IPM_TRACE_BLOCK=b),
+# loaded with IPM355_LIB=build/trace/libipm355_trace.so (scripts/role_trace.py)
+TRACE_OUT := build/trace/libipm355_trace.so
+trace: $(TRACE_OUT)
+$(TRACE_OUT): $(SRCS) $(HDRS)
+	@mkdir -p build/trace
+	$(HIPCC) $(HIPFLAGS) -DIPM_ROLE_TRACE -c $(SRC_DIR)/ipm_blas.hip -o build/trace/ipm_blas.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC build/trace/ipm_blas.o $(OBJ_DIR)/ipm_barrier.o \
+	    $(OBJ_DIR)/ipm_engine.o -o $@
+
 clean:
 	rm -rf build $(OUT)
 
-.PHONY: all clean
+.PHONY: all clean trace

@@ -214,14 +214,6 @@ constexpr int PF_RB = 64;    // rows per TRSM workgroup
 constexpr int CH_NB = IPM_CH_NB;   // outer block (trailing-update depth)
 constexpr int PF_DINV = 8 * 256;  // workspace doubles: the eight Dinv blocks, then the packed L11 (36 blocks)
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ unsigned ld_ctl(unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -235,11 +227,86 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
+// acc -= x[lane l of this 16-lane row] * x  (one v_fmac_f64 with a DPP row broadcast of src0;
+// gfx90a+ DPP64 supports row_newbcast).  l must fold to a constant.  nop: the first use of a
+// freshly written x carries the s_nop of the DPP read-after-VALU-write hazard in the same asm
+// statement (the compiler cannot move the producer between them).
+__device__ __forceinline__ void fmac_bcast16(double& acc, double x, int l, bool nop = false) {
+  switch (l) {
+    case 0:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 1:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 2:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 3:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 4:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 5:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 6:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 7:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 8:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 9:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 10:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 11:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 12:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 13:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 14:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+    case 15:
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      break;
+  }
+}
+
 #ifdef IPM_STAMPS
-__device__ unsigned long long ipm_stamps[64];
+__device__ unsigned long long ipm_stamps[128];
 #define STAMP() do { if (tid == 0) ipm_stamps[nst] = __builtin_amdgcn_s_memtime(); ++nst; } while (0)
+#define STAMPAT(i) do { if (lane == 0) ipm_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP() do {} while (0)
+#define STAMPAT(i) do {} while (0)
 #endif
 
 // 1/sqrt(x) for the Cholesky pivots (x > 0, normal): v_rsq_f64 plus one third-order correction
@@ -286,23 +353,30 @@ struct DiagSmem {
   double sD[36 * 256];   // L11 (identity-padded beyond nb)
   double sLr[256];       // L_JJ row-major (broadcast reads of its rows)
   double srinv[8 * 16];  // 1 / L_cc per diagonal block
-  double scol[2][16];    // leaf column broadcast
   int fail;
 };
 
+// FUSED: inside the one-launch-per-block factorisation (k_potrf_block): the panel was written by
+// other workgroups of the same launch (sc1 loads), and failures are also recorded in *failw.
+template <bool FUSED = false>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
                                           double* __restrict__ dinv_out, int* __restrict__ info,
-                                          double* pubL, unsigned* progress, DiagSmem& sm) {
+                                          double* pubL, unsigned* progress, DiagSmem& sm,
+                                          unsigned* failw = nullptr) {
   double* sD = sm.sD;
   double* sLr = sm.sLr;
   double* srinv = sm.srinv;
-  auto& scol = sm.scol;
   int& fail = sm.fail;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 4 waves
   const int fr = lane & 15, fk = lane >> 4;
 #ifdef IPM_STAMPS
   int nst = 0;
 #endif
+#ifndef IPM_DIAG_PRIO
+#define IPM_DIAG_PRIO 3
+#endif
+  // the diagonal chain is the critical path; its CU-mates are trailing-update tiles
+  if (FUSED && IPM_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(IPM_DIAG_PRIO);
   if (tid == 0) fail = 0;
   STAMP();
   const int i0 = 2 * (tid & 63), jb = tid >> 6;
@@ -322,9 +396,9 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
             const double* src = A + (k0 + J * 16 + (lane >> 3) + 8 * h) * lda + k0 + I * 16 + 2 * (lane & 7);
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                              (__attribute__((address_space(3))) void*)&sD[bidx(I, J) * 256 + h * 128],
-                                             16, 0, 0);
+                                             16, 0, FUSED ? 16 : 0);   // aux 16 = sc1
           }
-    if (*info != 0) return;
+    if (!FUSED && *info != 0) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     // ---- partial panel (last one): register path with identity padding beyond nb
@@ -332,7 +406,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     const int ic0 = min(i0, nb - 1), ic1 = min(i0 + 1, nb - 1);
     const double* base = A + k0 * lda + k0;
     double2 v[32];
-    if (vec && i0 + 1 < nb) {
+    if (!FUSED && vec && i0 + 1 < nb) {
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
         const int jc = min(jb + 4 * q, nb - 1);
@@ -342,11 +416,11 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
         const int jc = min(jb + 4 * q, nb - 1);
-        v[q].x = base[jc * lda + ic0];
-        v[q].y = base[jc * lda + ic1];
+        v[q].x = FUSED ? ld_sc1(base + jc * lda + ic0) : base[jc * lda + ic0];
+        v[q].y = FUSED ? ld_sc1(base + jc * lda + ic1) : base[jc * lda + ic1];
       }
     }
-    if (*info != 0) return;
+    if (!FUSED && *info != 0) return;
 #pragma unroll
     for (int q = 0; q < 32; ++q) {
       const int j = jb + 4 * q;
@@ -360,32 +434,67 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   }
   __syncthreads();
   STAMP();
-  for (int J = 0; J < 8; ++J) {
-    // ---- 1. left-looking update of block column J: T_IJ -= sum_{P<J} L_IP L_JP^T, I >= J
-    //      wave 0 updates the diagonal tile and goes straight on to factor it; waves 1-3 update
-    //      the tiles below meanwhile (no barrier in between)
-    for (int tI = (wv == 0 ? 0 : wv); J > 0 && tI < 8 - J; tI += (wv == 0 ? 8 : 3)) {
-      const int I = J + tI;
-      const int cb = bidx(I, J) * 256 + fk * 16 + fr;
-      dbl4 acc[4];
+  // T_IK -= L_IP L_KP^T on one 16 x 16 tile (transposed MFMA layout, see above)
+  auto tile_update = [&](int I, int K, int P) {
+    const int cb = bidx(I, K) * 256 + fk * 16 + fr;
+    const int ab = bidx(K, P) * 256 + fk * 16 + fr, bb = bidx(I, P) * 256 + fk * 16 + fr;
+    dbl4 acc;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < 4; ++r) acc[r] = sD[cb + 64 * r];
+    double av[4], bv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[0][r] = sD[cb + 64 * r];
-      for (int P = 0; P < J; ++P) {
-        const int ab = bidx(J, P) * 256 + fk * 16 + fr, bb = bidx(I, P) * 256 + fk * 16 + fr;
-        double av[4], bv[4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          av[s4] = -sD[ab + 64 * s4];
-          bv[s4] = sD[bb + 64 * s4];
-        }
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[s4], 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+    for (int s4 = 0; s4 < 4; ++s4) {
+      av[s4] = -sD[ab + 64 * s4];
+      bv[s4] = sD[bb + 64 * s4];
     }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = acc[r];
+  };
+  // T_IK -= sum_{P < np} L_IP L_KP^T (two accumulators)
+  auto tile_update_n = [&](int I, int K, int np) {
+    const int o = fk * 16 + fr, cb = bidx(I, K) * 256 + o;
+    dbl4 x0, x1 = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x0[r] = sD[cb + 64 * r];
+    for (int P = 0; P < np; ++P) {
+      const int ab = bidx(K, P) * 256 + o, bb = bidx(I, P) * 256 + o;
+      double av[4], bv[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        av[s4] = -sD[ab + 64 * s4];
+        bv[s4] = sD[bb + 64 * s4];
+      }
+      x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0], bv[0], x0, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1], bv[1], x1, 0, 0, 0);
+      x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[2], bv[2], x0, 0, 0, 0);
+      x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[3], bv[3], x1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = x0[r] + x1[r];
+  };
+  // final block column Jc of L11 -> A (lower part of the diagonal tile; i, j < nb); tiles
+  // I = Jc + part, Jc + part + parts, ...
+  auto write_back = [&](int Jc, int part, int parts) {
+    for (int I = Jc + part; I < 8; I += parts) {
+      const int cb = bidx(I, Jc) * 256;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = fk + 4 * q, i = I * 16 + fr, j = Jc * 16 + c;
+        if (i < nb && j < nb && (I > Jc || fr >= c)) A[(k0 + j) * lda + k0 + i] = sD[cb + c * 16 + fr];
+      }
+    }
+  };
+  // Left-looking with one block column of look-ahead: term P (block column P of L, final after
+  // step 3 of iteration P) reaches block column P+1 in step 1 of iteration P+1 (4 MFMAs per
+  // tile; for the diagonal tile that is all the chain waits for); block column J+1 receives
+  // terms 0..J-1 during the leaf of iteration J (waves 1-2, off the chain).
+  for (int J = 0; J < 8; ++J) {
+    // ---- 1. term J-1 on block column J: wave 0 the diagonal tile (then straight on to factor
+    //      it), waves 1-3 the tiles below
+    if (J > 0)
+      for (int tI = (wv == 0 ? 0 : wv); tI < 8 - J; tI += (wv == 0 ? 8 : 3)) tile_update(J + tI, J, J - 1);
     STAMP();
     // ---- 2. wave 0: factor the 16 x 16 block (J,J) in registers, lane r = row r.
     //      Right-looking with NO lane masks: entries above the diagonal (lane r < column c)
@@ -398,34 +507,61 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
       for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
       // Column c+1 is updated first (readlane broadcast) and ITS pivot's rsqrt issued; the rest of
-      // column c's rank-1 update reads column c from an LDS copy (one write, four 32-byte reads
-      // instead of 2 readlanes per element) and fills the rsqrt latency.
-      // Column c+1 is updated first (readlane broadcast) and ITS pivot's rsqrt issued; the rest of
       // column c's rank-1 update reads column c from an LDS copy (one write, a few wide reads
       // instead of 2 readlanes per element) and fills the rsqrt latency.
       int bad = 0;
       double piv = readlane_d(row[0], 0);
       double dv = rsqrt_pivot(piv);
       double dvs[16];
+#ifndef IPM_LEAF
+#define IPM_LEAF 4
+#endif
+#if IPM_LEAF == 4
+      // pivot chain kept minimal: the next pivot is formed from two values read BEFORE this
+      // column is scaled, l = A[c+1][c] dv_c, piv' = A[c+1][c+1] - l^2 (bitwise what the vector
+      // update leaves in lane c+1), so dv_c -> dv_{c+1} is mul, fma, rsqrt; the column scaling
+      // and the rank-1 updates (one v_fmac_f64 with DPP row broadcast each) run beside it
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        dvs[c] = dv;
+        double pivn = 1.0, dvn = 1.0;
+        if (c + 1 < 16) {
+          const double a1 = readlane_d(row[c], c + 1);
+          const double d1 = readlane_d(row[c + 1], c + 1);
+          const double l1 = a1 * dv;
+          pivn = fma(-l1, l1, d1);
+          dvn = rsqrt_pivot(pivn);
+        }
+        row[c] *= dv;                      // lane c: piv * dv = L_cc
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) fmac_bcast16(row[c2], row[c], c2, c2 == c + 1);
+        piv = pivn;
+        dv = dvn;
+      }
+#else
+      // column c's entries L[c2][c] go to scalar registers (v_readlane, all independent); the next
+      // column is updated and its pivot's rsqrt issued first, the other updates fill its latency
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         if (!(piv > 0.0) && bad == 0) bad = c + 1;
         dvs[c] = dv;
         row[c] *= dv;                      // lane c: piv * dv = L_cc
-        scol[c & 1][rr] = row[c];          // lanes 16-63 duplicate rows: same value, same address
+        double l[16];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) l[c2] = readlane_d(row[c], c2);
         double pivn = 1.0, dvn = 1.0;
         if (c + 1 < 16) {
-          row[c + 1] = fma(-row[c], readlane_d(row[c], c + 1), row[c + 1]);
+          row[c + 1] = fma(-row[c], l[c + 1], row[c + 1]);
           pivn = readlane_d(row[c + 1], c + 1);
           dvn = rsqrt_pivot(pivn);
         }
-        // (same-wave LDS write -> read: in order, no barrier needed; the compiler keeps the order
-        //  because the addresses may alias)
 #pragma unroll
-        for (int c2 = c + 2; c2 < 16; ++c2) row[c2] = fma(-row[c], scol[c & 1][c2], row[c2]);
+        for (int c2 = c + 2; c2 < 16; ++c2) row[c2] = fma(-row[c], l[c2], row[c2]);
         piv = pivn;
         dv = dvn;
       }
+#endif
       if (lane < 16) {
 #pragma unroll
         for (int c = 0; c < 16; ++c)
@@ -440,15 +576,23 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         }
       }
       if (lane == 0 && bad) fail = J * 16 + bad;
+      STAMPAT(32 + J);
     } else if (wv == 3 && J > 0) {
       // meanwhile (off the chain) wave 3 inverts the PREVIOUS diagonal block for the row part
       tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
                     pubL != nullptr);
-    } else if (wv == 2 && J > 0 && pubL) {
-      // ... and wave 2 publishes the previous diagonal block (the chain wave stores nothing)
-      const int db = bidx(J - 1, J - 1) * 256;
+      STAMPAT(40 + J);
+    } else if (J > 0) {
+      // waves 1-2: wave 2 publishes the previous diagonal block; both apply terms 0..J-1 to the
+      // tiles of block column J+1 (look-ahead)
+      if (wv == 2 && pubL) {
+        const int db = bidx(J - 1, J - 1) * 256;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
+        for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
+      }
+      STAMPAT(64 + 8 * wv + J);
+      for (int I = J + wv; I < 8; I += 2) tile_update_n(I, J + 1, J);
+      STAMPAT(80 + 8 * wv + J);
     }
     if (pubL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -458,6 +602,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     if (pubL && tid == 0 && J > 0) __hip_atomic_store(progress, (unsigned)J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- 3. tiles below: X = T L_JJ^-T by substitution, one thread per tile row:
     //      X[r][c] = (T[r][c] - sum_{k<c} X[r][k] L[c][k]) / L_cc
+    if (J > 0 && wv >= 2) write_back(J - 1, wv - 2, 2);   // (step 3 needs at most 112 threads)
     if (tid < (7 - J) * 16) {
       const int I = J + 1 + (tid >> 4), r = tid & 15;
       const int cb = bidx(I, J) * 256 + r;
@@ -484,6 +629,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   if (fail) {
     if (tid == 0) {
       atomicCAS(info, 0, (int)(k0 + fail));
+      if (failw) atomicCAS(failw, 0u, (unsigned)(k0 + fail));
       // release the row workgroups (they finish on garbage; the failed factor is discarded)
       if (pubL) {
         __threadfence();
@@ -498,23 +644,11 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
     for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
   }
+  if (wv == 1) write_back(7, 0, 1);   // (block columns 0..6 went back during the loop)
   if (pubL) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_store(progress, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // ---- write back L11 (lower part, i < nb, j < nb)
-  {
-    double* col = A + k0 * lda + k0 + i0;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const int j = jb + 4 * q;
-      if ((i0 >> 4) >= (j >> 4) && j < nb) {
-        const double2 v = *reinterpret_cast<const double2*>(&sD[bidx(i0 >> 4, j >> 4) * 256 + (j & 15) * 16 + (i0 & 15)]);
-        if (i0 >= j && i0 < nb) col[j * lda] = v.x;
-        if (i0 + 1 >= j && i0 + 1 < nb) col[j * lda + 1] = v.y;
-      }
-    }
   }
   STAMP();
 }
@@ -525,9 +659,13 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 //   X_J = (B_J - sum_{P<J} X_P L_JP^T) Dinv_J^T,
 // starting step J as soon as the diagonal role has released block row J (*progress > J).
 // L blocks and Dinv come from the producer's sc1 stores and are read with sc1 loads only.
+// FUSED: as for diag_role; *done (if given) is set once this chunk's rows (and its part of the
+// next panel's columns) are stored.
+template <bool FUSED = false>
 __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, int nb, double* __restrict__ A,
                                          int64_t lda, const double* dinv, const double* pubL,
-                                         unsigned* progress) {
+                                         unsigned* progress, int next_nb, unsigned* nextc, double* stage,
+                                         int* sflag, unsigned* done = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int64_t row = k0 + nb + chunk * PF_RB + wv * 16 + fr;
@@ -539,7 +677,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int c = J * 16 + fk + 4 * r;
-      b[J][r] = (rin && c < nb) ? A[(k0 + c) * lda + row] : 0.0;
+      b[J][r] = (rin && c < nb) ? (FUSED ? ld_sc1(&A[(k0 + c) * lda + row]) : A[(k0 + c) * lda + row]) : 0.0;
     }
   dbl4 x[8];
   unsigned known = 0;
@@ -568,25 +706,104 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
     for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(dvv[s4], acc[s4], xj, 0, 0, 0);
     x[J] = xj;
   }
+  // rows of the next panel's diagonal block are handed to the other workgroups of this launch
+  const int nchd = (next_nb + PF_RB - 1) / PF_RB;
+  const bool pub = chunk < nchd;
   if (rin) {
 #pragma unroll
     for (int J = 0; J < 8; ++J)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = J * 16 + fk + 4 * r;
-        if (c < nb) A[(k0 + c) * lda + row] = x[J][r];
+        if (c < nb) {
+          if (pub) st_sc1(&A[(k0 + c) * lda + row], x[J][r]);
+          else A[(k0 + c) * lda + row] = x[J][r];
+        }
       }
+  }
+  if (next_nb > 0) {
+  // ---- fused intra-block update (replaces a GEMM launch between the two panels of a block):
+  //   A[rows, k0+nb : k0+nb+next_nb] -= X[rows, :] L[k0+nb : k0+nb+next_nb, k0 : k0+nb]^T
+  // (nb == 128 here).  The second factor is this panel's result for the first nchd row chunks.
+  if (pub) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(nextc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) {
+    int ok = 1;
+    while (ld_ctl(nextc) < (unsigned)nchd) {
+      if (ld_ctl(progress) == 0xFFFFFFFFu) { ok = 0; break; }   // diagonal failed: info is set
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *sflag = ok;
+  }
+  __syncthreads();
+  constexpr int SLAB = 128 * 16 + 16;   // one 16-row slab of the second factor, k-major (+ bank pad)
+#pragma unroll 1
+  for (int h = 0; h < 2 && *sflag; ++h) {
+    if (64 * h >= next_nb) break;
+    if (h) __syncthreads();
+    {
+      // thread (k = wv + 4q, jj = lane): 512 contiguous bytes per wave and k
+      const bool jin = 64 * h + lane < next_nb;
+      const double* src = A + (k0 + wv) * lda + k0 + nb + 64 * h + lane;
+      double* dst = stage + (lane >> 4) * SLAB + wv * 16 + (lane & 15);
+#pragma unroll 1
+      for (int q0 = 0; q0 < 32; q0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = jin ? ld_sc1(src + (int64_t)(4 * (q0 + q)) * lda) : 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dst[(q0 + q) * 64] = v[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int jl = 0; jl < 4; ++jl) {
+      const int jt = 4 * h + jl;
+      if (16 * jt >= next_nb) break;
+      const int64_t col0 = k0 + nb + 16 * jt;
+      dbl4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[r] = (rin && 16 * jt + fk + 4 * r < next_nb)
+                     ? (FUSED ? ld_sc1(&A[(col0 + fk + 4 * r) * lda + row]) : A[(col0 + fk + 4 * r) * lda + row])
+                     : 0.0;
+      const double* sb = stage + jl * SLAB + fk * 16 + fr;
+#pragma unroll
+      for (int P = 0; P < 8; ++P)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-sb[(16 * P + 4 * s4) * 16], x[P][s4], acc, 0, 0, 0);
+      if (rin) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * jt + fk + 4 * r < next_nb) {
+            if (FUSED) st_sc1(&A[(col0 + fk + 4 * r) * lda + row], acc[r]);
+            else A[(col0 + fk + 4 * r) * lda + row] = acc[r];
+          }
+      }
+    }
+  }
+  }   // next_nb > 0
+  if (done) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // One panel (width nb <= 128 at column k0) in ONE launch.  Workgroups draw tickets: ticket 0 is the
 // diagonal role (so it is resident before anyone waits on it -- no deadlock for any residency),
 // tickets 1.. are the row chunks, pipelined one block column behind the diagonal role.
-// ctl: 2 zeroed words {ticket, progress}.
-__global__ __launch_bounds__(256) void k_potrf_panel(int64_t n, int64_t k0, int nb, double* __restrict__ A,
-                                                     int64_t lda, double* ws, unsigned* ctl, int* __restrict__ info) {
+// next_nb > 0 (nb == 128): the row chunks also apply this panel to the next panel's columns.
+// ctl: 4 zeroed words {ticket, progress, next-diagonal rows published, -}.
+__global__ __launch_bounds__(256, 2) void k_potrf_panel(int64_t n, int64_t k0, int nb, int next_nb,
+                                                     double* __restrict__ A, int64_t lda, double* ws, unsigned* ctl,
+                                                     int* __restrict__ info) {
   __shared__ DiagSmem sm;
-  __shared__ int sticket;
+  __shared__ int sticket, sflag;
   if (threadIdx.x == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
   __syncthreads();
   const int t = sticket;
@@ -596,16 +813,338 @@ __global__ __launch_bounds__(256) void k_potrf_panel(int64_t n, int64_t k0, int 
     diag_role(k0, nb, A, lda, dinv, info, pubL, &ctl[1], sm);
   } else {
     if (*info != 0) return;
-    row_role(t - 1, n, k0, nb, A, lda, dinv, pubL, &ctl[1]);
+    row_role(t - 1, n, k0, nb, A, lda, dinv, pubL, &ctl[1], next_nb, &ctl[2], sm.sD, &sflag);
   }
 }
 
-// one panel of width nb <= 128 at column k0 (ctl: this panel's 2 zeroed control words)
+// one panel of width nb <= 128 at column k0 (ctl: this panel's 4 zeroed control words);
+// next_nb > 0 requires nb == 128 and k0 + nb + next_nb <= n
 static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info,
-                         double* ws, unsigned* ctl) {
+                         double* ws, unsigned* ctl, int next_nb = 0) {
   const int64_t below = n - k0 - nb;
   hipLaunchKernelGGL(k_potrf_panel, dim3(1 + cdiv(std::max<int64_t>(below, 0), PF_RB)), dim3(256), 0, st, n, k0,
-                     nb, A, lda, ws, ctl, info);
+                     nb, next_nb, A, lda, ws, ctl, info);
+}
+// fused intra-block update in the first panel of a block (IPM_NO_FOLD=1: separate GEMM launch)
+static bool fold_intra() {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("IPM_NO_FOLD");
+    f = (e && atoi(e) == 1) ? 0 : 1;
+  }
+  return f == 1;
+}
+
+// =====================================================================================
+// One launch per 256-column block (default path).  Block b = columns [cb, cb + wa + wbw):
+//   LA  tiles : A[cb:n, block b] -= L[cb:n, block b-1] L[block b, block b-1]^T   (64-tiles,
+//               row blocks in order; la_done[row block] counts finished tiles)
+//   P(a)      : panel [cb, cb+wa): diagonal role, then row chunks; the row chunks also apply
+//               P(a) to P(b)'s columns (fold) and set pa_done[chunk]
+//   P(b)      : panel [cb+wa, cb+wa+wbw) (waits for pa_done of the chunks holding its rows)
+//   S   tiles : A[cb+wb:n, cb+wb:n] -= L[.., block b-1] L[.., block b-1]^T  (128-tiles, lower)
+// Workgroups take TICKETS in this order and only ever wait for lower tickets, so the launch
+// cannot deadlock for any residency (and not beside other launches either).  Everything one
+// workgroup hands to another inside the launch moves with sc1 loads/stores.
+// The panel work of block b thus overlaps the trailing update of block b-1 in ONE stream: no
+// cross-stream event waits (~10 us each on this platform).
+// =====================================================================================
+struct BlockArgs {
+  int64_t n = 0, lda = 0;
+  double* A = nullptr;
+  int* info = nullptr;
+  double* wsA = nullptr;        // P(a): Dinv (PF_DINV) + packed L11 (36 blocks)
+  double* wsB = nullptr;        // P(b): same
+  unsigned* ctl = nullptr;      // this launch's zeroed control words (CTL_* below)
+  const unsigned* prevfail = nullptr;   // failure word of the previous launch
+  int64_t cb = 0;
+  int wa = 0, wbw = 0;
+  int nla = 0, nra = 0, nrb = 0, la_tj = 0, nlab = 0;
+  int64_t ns = 0;
+  GemmArgs la, s;
+  int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
+};
+enum {
+  CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
+  CTL_PA_CU = 5, CTL_PB_CU = 6,   // 1 + CU key of the diagonal roles' workgroups
+  CTL_SPILL_A = 7, CTL_SPILL_B = 8,   // 1 + a trailing tile handed off by a workgroup on a diag CU
+  CTL_HDR = 16
+};
+
+// this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
+__device__ __forceinline__ unsigned cu_key() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  return ((xcc & 15u) << 8) | ((hw >> 8) & 0xFFu);
+}
+// control words per launch (block_ctl_words, ipm_common.h): header, la_done[ceil(n/64)],
+// pa_done[ceil(n/64)]
+
+// trailing tiles dispatched after the P(a) / P(b) row chunks (see the ticket order in k_potrf_block)
+#ifndef IPM_S_TAIL1
+#define IPM_S_TAIL1 0
+#endif
+#ifndef IPM_S_TAIL2
+#define IPM_S_TAIL2 0
+#endif
+constexpr int64_t S_TAIL1 = IPM_S_TAIL1, S_TAIL2 = IPM_S_TAIL2;
+
+union BlockSmem {
+  DiagSmem d;
+  MfSmem<128, 2> g128;
+  MfSmem<64, 2> g64;
+};
+
+// thread 0 waits until words w[0..cnt) are all >= target; then the workgroup proceeds
+__device__ __forceinline__ void wait_words(unsigned* w, int cnt, unsigned target) {
+  if (threadIdx.x == 0)
+    for (int i = 0; i < cnt; ++i)
+      while (ld_ctl(w + i) < target) __builtin_amdgcn_s_sleep(2);
+  __syncthreads();
+}
+
+#ifdef IPM_ROLE_TRACE
+// diagnostic build only: per workgroup of the traced launch {ticket | role << 32, start, end}
+// in s_memrealtime ticks (100 MHz)
+__device__ unsigned long long ipm_role_trace[8192 * 4];
+struct RoleTrace {
+  bool on;
+  int ticket;
+  unsigned long long t0;
+  int role = -1;
+  __device__ RoleTrace(bool o, int t) : on(o && t < 8192), ticket(t), t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~RoleTrace() {
+    if (on && threadIdx.x == 0) {
+      ipm_role_trace[4 * ticket] = (unsigned long long)(unsigned)ticket | ((unsigned long long)(unsigned)role << 32);
+      ipm_role_trace[4 * ticket + 1] = t0;
+      ipm_role_trace[4 * ticket + 2] = __builtin_amdgcn_s_memrealtime();
+      ipm_role_trace[4 * ticket + 3] = cu_key();
+    }
+  }
+};
+#define ROLE(r) (rt.role = (r))
+#else
+#define ROLE(r) ((void)0)
+#endif
+
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
+  __shared__ BlockSmem sm;
+  __shared__ int sticket, sflag;
+  const int tid = threadIdx.x;
+  if (tid == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
+  __syncthreads();
+  int64_t t = sticket;
+#ifdef IPM_ROLE_TRACE
+  RoleTrace rt(b.trace != 0, (int)t);
+#endif
+  {
+    // a failure in an earlier launch: pass it on and stop (consistent for every workgroup:
+    // the word was final before this launch started)
+    const unsigned pf = ld_ctl(const_cast<unsigned*>(b.prevfail));
+    if (pf != 0) {
+      if (t == 0 && tid == 0) __hip_atomic_store(&b.ctl[CTL_FAIL], pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+  unsigned* la_done = b.ctl + CTL_HDR;
+  unsigned* pa_done = la_done + (b.n + 63) / 64;
+  if (t < b.nla) {
+    ROLE(0);
+    mfma_tile<64, false, VEC, 2, true>(b.la, t, sm.g64);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&la_done[t / b.la_tj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  t -= b.nla;
+  const unsigned lat = (unsigned)b.la_tj;
+  // LA row blocks [r0/64, r1/64] (rows relative to cb) finished
+  auto wait_la = [&](int64_t r0, int64_t r1) {
+    if (b.nla == 0) return;
+    const int64_t q0 = r0 / 64, q1 = std::min<int64_t>(r1 / 64, b.nlab - 1);
+    wait_words(la_done + q0, (int)(q1 - q0 + 1), lat);
+  };
+  const int64_t k1 = b.cb + b.wa;
+  // ticket order after the LA tiles: P(a) diagonal, the P(a) row chunks P(b)'s diagonal block
+  // needs (nchd), P(b) diagonal, S tiles, the other P(a) row chunks, P(b) row chunks.  Row chunks
+  // spin while their diagonal role works; dispatched after the S tiles they do not hold slots
+  // the trailing update could use.  Decode first, then ONE call site per role (each role's code
+  // is inlined once: register pressure and code size).
+  const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
+  enum { K_DIAG, K_ROW, K_TILE, K_NONE } kind = K_NONE;
+  bool pb = false;       // the role belongs to P(b)
+  int64_t chunk = 0;
+  if (t == 0) {
+    kind = K_DIAG;
+  } else if ((t -= 1) < nchd) {
+    kind = K_ROW;
+    chunk = t;
+  } else {
+    t -= nchd;
+    if (b.wbw > 0 && t == 0) {
+      kind = K_DIAG;
+      pb = true;
+    } else {
+      // [S seg 0][P(a) rows >= nchd][S seg 1][P(b) rows][S seg 2]: the row chunks are dispatched
+      // while the last tiles run (their diagonal roles are done by then) instead of after them
+      if (b.wbw > 0) t -= 1;
+      const int64_t s2 = std::min<int64_t>(b.ns, S_TAIL2), s1 = std::min<int64_t>(b.ns - s2, S_TAIL1);
+      const int64_t s0 = b.ns - s1 - s2;
+      const int64_t na = b.nra - nchd;
+      if (t < s0) {
+        kind = K_TILE;
+      } else if ((t -= s0) < na) {
+        kind = K_ROW;
+        chunk = nchd + t;
+      } else if ((t -= na) < s1) {
+        kind = K_TILE;
+        t += s0;
+      } else if ((t -= s1) < b.nrb) {
+        kind = K_ROW;
+        pb = true;
+        chunk = t;
+      } else if ((t -= b.nrb) < s2) {
+        kind = K_TILE;
+        t += s0 + s1;
+      }
+    }
+  }
+  double* ws = pb ? b.wsB : b.wsA;
+  unsigned* prog = &b.ctl[pb ? CTL_PB_PROG : CTL_PA_PROG];
+  const int64_t kp = pb ? k1 : b.cb;
+  const int nbp = pb ? b.wbw : b.wa;
+  if (kind == K_DIAG) {
+    ROLE(pb ? 3 : 1);
+    if (tid == 0)
+      __hip_atomic_store(&b.ctl[pb ? CTL_PB_CU : CTL_PA_CU], 1u + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pb) wait_words(pa_done, nchd, 1u);
+    else wait_la(0, b.wa - 1);
+    diag_role<true>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
+    return;
+  }
+  if (kind == K_ROW) {
+    ROLE(pb ? 6 : (chunk < nchd ? 2 : 5));
+    if (pb) {
+      // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
+      const int64_t r0 = b.wbw + chunk * PF_RB;
+      const int64_t q1 = std::min<int64_t>((std::min<int64_t>(r0 + PF_RB, b.n - k1) - 1) / PF_RB, b.nra - 1);
+      wait_words(pa_done + r0 / PF_RB, (int)(q1 - r0 / PF_RB + 1), 1u);
+    } else {
+      const int64_t r0 = b.wa + chunk * PF_RB;
+      wait_la(r0, std::min<int64_t>(r0 + PF_RB, b.n - b.cb) - 1);
+    }
+    row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
+                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk]);
+    return;
+  }
+  if (kind == K_TILE) {
+    ROLE(4);
+    // A trailing tile that lands on the CU of a running diagonal role (the critical chain) hands
+    // its tile to the spill word of that role and sleeps, keeping the slot so that no MFMA tile
+    // shares the CU with the chain.  Every tile workgroup, after its own tile, takes what is in
+    // the spill words; the sleeper, once the role is done, runs its tile itself if nobody took it.
+    unsigned* spill[2] = {&b.ctl[CTL_SPILL_A], &b.ctl[CTL_SPILL_B]};
+    unsigned* dprog[2] = {&b.ctl[CTL_PA_PROG], &b.ctl[CTL_PB_PROG]};
+    if (tid == 0) {
+      const unsigned me = 1u + cu_key();
+      int q = -1;
+      if (ld_ctl(&b.ctl[CTL_PA_CU]) == me && ld_ctl(dprog[0]) < 8u) q = 0;
+      else if (ld_ctl(&b.ctl[CTL_PB_CU]) == me && ld_ctl(dprog[1]) < 8u) q = 1;
+      if (q >= 0) {
+        ROLE(7 + q);
+        __hip_atomic_store(spill[q], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (ld_ctl(dprog[q]) < 8u) __builtin_amdgcn_s_sleep(20);   // 0xFFFFFFFF (failure) ends it too
+        sflag = (int)__hip_atomic_exchange(spill[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        sflag = (int)(t + 1);
+      }
+    }
+    // own tile, then the two spill words (one tile call site: the tile code is inlined once)
+#pragma nounroll
+    for (int q = -1; q < 2; ++q) {
+      if (q >= 0 && tid == 0)
+        sflag = (int)__hip_atomic_exchange(spill[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int v = sflag;
+      __syncthreads();
+      if (v) mfma_tile<128, false, VEC, 2, false>(b.s, v - 1, sm.g128);
+    }
+  }
+}
+
+// workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
+static constexpr int64_t PANEL_WS = PF_DINV + 36 * 256;
+
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
+  hipMemsetAsync(info, 0, sizeof(int), st);
+  if (n <= 0) return;
+  const int64_t nblocks = cdiv(n, CH_NB), cw = block_ctl_words(n);
+  unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
+  // word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
+  hipMemsetAsync(ctl0, 0, sizeof(unsigned) * (8 + nblocks * cw), st);
+  const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
+  for (int64_t bk = 0; bk < nblocks; ++bk) {
+    BlockArgs b;
+    b.n = n;
+    b.lda = lda;
+    b.A = A;
+    b.info = info;
+    b.wsA = ws;
+    b.wsB = ws + PANEL_WS;
+    b.ctl = ctl0 + 8 + bk * cw;
+    b.prevfail = bk == 0 ? ctl0 : ctl0 + 8 + (bk - 1) * cw + CTL_FAIL;
+    const int64_t cb = bk * CH_NB, wb = std::min<int64_t>(CH_NB, n - cb);
+    b.cb = cb;
+    b.wa = (int)std::min<int64_t>(wb, PF_NB);
+    b.wbw = (int)(wb - b.wa);
+    if (bk > 0) {
+      const int64_t cp = cb - CH_NB;
+      GemmArgs& a = b.la;
+      a.ni = n - cb;
+      a.nj = wb;
+      a.K = CH_NB;
+      a.X = a.Y = A + cp * lda + cb;
+      a.ldx = a.ldy = lda;
+      a.C = A + cb * lda + cb;
+      a.ldc = lda;
+      a.sub = 1;
+      a.rowmajor = 1;
+      a.xcd_remap = 0;
+      a.tiles_i = cdiv(a.ni, 64);
+      a.tiles_j = cdiv(a.nj, 64);
+      a.nblk = a.tiles_i * a.tiles_j;
+      b.nla = (int)a.nblk;
+      b.la_tj = (int)a.tiles_j;
+      b.nlab = (int)a.tiles_i;
+      const int64_t m = n - cb - wb;
+      if (m > 0) {
+        GemmArgs& g = b.s;
+        g.ni = g.nj = m;
+        g.K = CH_NB;
+        g.X = g.Y = A + cp * lda + cb + wb;
+        g.ldx = g.ldy = lda;
+        g.C = A + (cb + wb) * lda + cb + wb;
+        g.ldc = lda;
+        g.sub = 1;
+        g.tri = 1;
+        g.tiles_i = cdiv(m, 128);
+        g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
+        b.ns = g.nblk;
+      }
+    }
+#ifdef IPM_ROLE_TRACE
+    {
+      static const int tb = [] { const char* e = getenv("IPM_TRACE_BLOCK"); return e ? atoi(e) : -1; }();
+      b.trace = bk == tb;
+    }
+#endif
+    b.nra = (int)cdiv(std::max<int64_t>(n - cb - b.wa, 0), PF_RB);
+    b.nrb = b.wbw > 0 ? (int)cdiv(std::max<int64_t>(n - cb - wb, 0), PF_RB) : 0;
+    const int64_t grid = b.nla + 1 + b.nra + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns;
+    if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
+  }
 }
 
 static int num_cus() {
@@ -635,9 +1174,15 @@ static int panel_reserve_cus() {
 // Without a side stream (side == main) the same sequence runs in order.
 void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
                     double* ws) {
+  // IPM_POTRF_LA=1: the earlier two-stream form below (kept for comparison); default: fused
+  static const bool two_stream = [] { const char* e = getenv("IPM_POTRF_LA"); return e && e[0] == '1'; }();
+  if (!two_stream) {
+    potrf_lower_fused(caller, n, A, lda, info, ws);
+    return;
+  }
   hipMemsetAsync(info, 0, sizeof(int), caller);
-  unsigned* ctl = reinterpret_cast<unsigned*>(ws + PF_DINV + 36 * 256);   // 2 words per panel
-  hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned) * cdiv(std::max<int64_t>(n, 1), PF_NB), caller);
+  unsigned* ctl = reinterpret_cast<unsigned*>(ws + PF_DINV + 36 * 256);   // 4 words per panel
+  hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned) * cdiv(std::max<int64_t>(n, 1), PF_NB), caller);
   const bool two = pst && pst->side;
   hipStream_t st = (two && pst->main) ? pst->main : caller;
   hipStream_t side = two ? pst->side : caller;
@@ -645,26 +1190,37 @@ void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, doub
   if (st != caller) { hipEventRecord(pst->ev_in, caller); hipStreamWaitEvent(st, pst->ev_in, 0); }
   if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
   hipStream_t ps = two ? side : st;
+  static const bool la_side = [] { const char* e = getenv("IPM_LA_SIDE"); return e && e[0] == '1'; }();
   for (int64_t k0 = 0; k0 < n; k0 += CH_NB) {
     const int w = (int)std::min<int64_t>(CH_NB, n - k0);
     // ---- panel k on the side stream
     const int w1 = std::min(w, PF_NB);
-    panel_launch(ps, n, k0, w1, A, lda, info, ws, ctl + 2 * (k0 / PF_NB));
+    const bool fold = w > w1 && fold_intra();
+    panel_launch(ps, n, k0, w1, A, lda, info, ws, ctl + 4 * (k0 / PF_NB), fold ? w - w1 : 0);
     if (w > w1) {
       // A[k0+w1 : n, k0+w1 : k0+w] -= L[k0+w1 : n, k0 : k0+w1] L[k0+w1 : k0+w, k0 : k0+w1]^T
-      gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
-                         A + (k0 + w1) * lda + k0 + w1, lda, info);
-      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws, ctl + 2 * ((k0 + w1) / PF_NB));
+      if (!fold)
+        gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
+                           A + (k0 + w1) * lda + k0 + w1, lda, info);
+      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws, ctl + 4 * ((k0 + w1) / PF_NB));
     }
     if (two) { hipEventRecord(ev_pan, side); hipStreamWaitEvent(st, ev_pan, 0); }
     // ---- trailing update on the main stream
     const int64_t r0 = k0 + w;
     if (r0 >= n) break;
     const int64_t w2 = std::min<int64_t>(CH_NB, n - r0);
-    // next block's columns (rectangle; its upper-triangle part is never read)
-    gemm_nt_sub_launch(st, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0, lda,
-                       info);
-    if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
+    // next block's columns (rectangle; its upper-triangle part is never read).  la_side: on the
+    // panel stream after the previous trailing update (ev_rel), so the next panel follows it
+    // without a stream hop.
+    if (two && la_side) {
+      hipStreamWaitEvent(side, ev_rel, 0);
+      gemm_nt_sub_launch(side, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0,
+                         lda, info);
+    } else {
+      gemm_nt_sub_launch(st, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0, lda,
+                         info);
+      if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
+    }
     if (n - r0 - w2 > 0) {
       GemmArgs a;
       a.ni = a.nj = n - r0 - w2;
@@ -683,9 +1239,17 @@ void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, doub
       if (two && res > 0) mfma_gemm_launch_persistent(st, a, num_cus() - res);
       else mfma_gemm_launch(st, a);
     }
+    if (two && la_side) hipEventRecord(ev_rel, st);
   }
   if (st != caller) { hipEventRecord(pst->ev_out, st); hipStreamWaitEvent(caller, pst->ev_out, 0); }
 }
+
+#ifdef IPM_ROLE_TRACE
+extern "C" int ipm_debug_role_trace(unsigned long long* out, int n_wg) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_role_trace), sizeof(unsigned long long) * 4 *
+                                                                       std::min(n_wg, 8192));
+}
+#endif
 
 void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
   potrf_lower_la(st, nullptr, n, A, lda, info, ws);

@@ -56,10 +56,16 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
                  const double* B, int64_t ldb, double* C, int64_t ldc);
 
 // Cholesky (column-major lower, in place). info_dev: device int (0 or first failing column, 1-based)
-// ws: device workspace of potrf_ws_doubles(n) doubles (the panel's inverted diagonal blocks,
-// the published L11 blocks, two control words per 128-column panel)
-inline int64_t potrf_ws_doubles(int64_t n) { return 8 * 256 + 36 * 256 + (n + 127) / 128 + 8; }
+// ws: device workspace of potrf_ws_doubles(n) doubles: two panels' inverted diagonal blocks and
+// published L11 blocks, then the control words (per launch: a header, one word per 64-row block
+// for the look-ahead tiles and one per 64-row chunk of the first panel)
+__host__ __device__ inline int64_t block_ctl_words(int64_t n) { return 16 + 2 * ((n + 63) / 64) + 8; }
+inline int64_t potrf_ws_doubles(int64_t n) {
+  return 2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8;
+}
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
+// one launch per 256-column block on stream s (the default behind potrf_lower / potrf_lower_la)
+void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
 // same with one block of look-ahead: panels on ps->side (high priority), trailing updates on
 // ps->main; both may be restricted to disjoint CU sets so the panel chain never waits for
 // trailing-update workgroups to drain.  ps == null or ps->side == null: everything in order on

@@ -440,10 +440,12 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
     if (!(nola && nola[0] == '1') &&
         hipStreamCreateWithPriority(&ps.side, hipStreamNonBlocking, greatest) != hipSuccess)
       ps.side = nullptr;
-    hipEventCreateWithFlags(&ps.ev_rel, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ps.ev_pan, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ps.ev_in, hipEventDisableTiming);
-    hipEventCreateWithFlags(&ps.ev_out, hipEventDisableTiming);
+    const char* nf = getenv("IPM_EV_NOFENCE");
+    const unsigned evf = hipEventDisableTiming | ((nf && nf[0] == '1') ? hipEventDisableSystemFence : 0u);
+    hipEventCreateWithFlags(&ps.ev_rel, evf);
+    hipEventCreateWithFlags(&ps.ev_pan, evf);
+    hipEventCreateWithFlags(&ps.ev_in, evf);
+    hipEventCreateWithFlags(&ps.ev_out, evf);
   }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }

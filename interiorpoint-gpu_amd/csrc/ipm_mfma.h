@@ -45,8 +45,19 @@ struct GemmArgs {
   int tri = 0;                   // lower-triangular tile grid (ni == nj), only i >= j written
   int sub = 0;                   // C -= acc  (alpha/beta/P/dvec ignored)
   int xcd_remap = 1;             // XCD-contiguous tile order (0: plain blockIdx order)
-  int64_t tiles_i = 0, nblk = 0;
+  int rowmajor = 0;              // tile L -> (L / tiles_j, L % tiles_j) (no remap): row blocks in order
+  int64_t tiles_i = 0, tiles_j = 0, nblk = 0;
 };
+
+// agent-coherent (sc1) element access: data handed between workgroups of ONE launch
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<unsigned long long*>(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // BM = 128 (4 x 4 MFMA tiles per wave) for large grids, 64 (2 x 2) when the 128-tile grid
 // would leave CUs idle.  WJ = waves along j (2: 256 threads, 2 workgroups per CU; 4: 512 threads).
@@ -63,23 +74,31 @@ struct MfCfg {
   static constexpr int TWJ = BM / (16 * WJ);  // ... along j (WJ waves)
 };
 
-template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
-__global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a) {
+// LDS of one tile: two K slabs of each operand
+template <int BM_, int WJ = 2>
+struct MfSmem {
+  double sX[2][MfCfg<BM_, WJ>::BK * MfCfg<BM_, WJ>::LD];
+  double sY[2][MfCfg<BM_, WJ>::BK * MfCfg<BM_, WJ>::LD];
+};
+
+// One output tile (index Lw of the launch's tile space) by one workgroup of 128 * WJ threads.
+// SC1OUT: the tile is stored with sc1 stores (read by other workgroups of the same launch).
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false>
+__device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
-  if (a.info && *a.info != 0) return;
-  __shared__ double sX[2][BK * LD];
-  __shared__ double sY[2][BK * LD];
-  __shared__ double spad[PAD > 0 ? PAD : 1];
-  if (PAD > 0 && a.ni < 0) spad[threadIdx.x] = 0.0;   // never executed: keeps the pad allocated
-  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
+  auto& sX = sm.sX;
+  auto& sY = sm.sY;
   // ---- tile of this workgroup
   int64_t bi, bj;
   {
     int64_t L = Lw;
     const int64_t q = a.nblk >> 3;
-    if (a.xcd_remap && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
-    if (a.tri) {
+    if (a.xcd_remap && !a.rowmajor && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
+    if (a.rowmajor) {
+      bi = L / a.tiles_j;
+      bj = L % a.tiles_j;
+    } else if (a.tri) {
       int64_t b = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
       while ((b + 1) * (b + 2) / 2 <= L) ++b;
       while (b * (b + 1) / 2 > L) --b;
@@ -206,7 +225,8 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
         if (i < a.ni && j < a.nj && (!a.tri || i >= j)) {
           double* cp = a.C + j * a.ldc + i;
           if (cinit) {
-            *cp = acc[tj][ti][r];
+            if (SC1OUT) st_sc1(cp, acc[tj][ti][r]);
+            else *cp = acc[tj][ti][r];
           } else {
             double v = a.alpha * acc[tj][ti][r];
             if (a.beta != 0.0) v += a.beta * (*cp);
@@ -217,7 +237,15 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
         }
       }
     }
-  }   // persistent tile loop
+}
+
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
+__global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a) {
+  if (a.info && *a.info != 0) return;
+  __shared__ MfSmem<BM_, WJ> sm;
+  __shared__ double spad[PAD > 0 ? PAD : 1];
+  if (PAD > 0 && a.ni < 0) spad[threadIdx.x] = 0.0;   // never executed: keeps the pad allocated
+  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
 }
 
 template <int BM>

@@ -1,0 +1,34 @@
+"""Role timeline of ONE fused Cholesky launch (block b) from the diagnostic library.
+   make trace && IPM_TRACE_BLOCK=b python scripts/role_trace.py [n]
+Prints, per role, count / first start / last end / mean duration (us from the launch's first start)."""
+import ctypes, os, sys
+os.environ.setdefault("IPM355_LIB", "/root/repo/build/trace/libipm355_trace.so")
+sys.path[:0] = ["/root/repo/interiorpoint-gpu_amd", "/root/repo/tests"]
+import numpy as np
+import torch
+from gpu_util import handle
+from ipm355 import _lib as L
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+h = handle()
+torch.manual_seed(0)
+M = torch.rand(n, n, dtype=torch.float64, device="cuda")
+A = M @ M.T + n * torch.eye(n, dtype=torch.float64, device="cuda")
+for _ in range(2):
+    Hc = A.clone(); torch.cuda.synchronize()
+    info = ctypes.c_int(0)
+    h.lib.ipm_potrf(h.ptr, n, L.dptr(Hc), n, ctypes.byref(info))
+    torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * (4 * 8192))()
+rc = h.lib.ipm_debug_role_trace(buf, 8192)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+a = a[a[:, 1] > 0]
+t0 = a[:, 1].min()
+names = {0: "LA tile", 1: "P(a) diag", 2: "P(a) row<nchd", 3: "P(b) diag", 4: "S tile", 5: "P(a) row", 6: "P(b) row",
+         7: "S sleep@Pa", 8: "S sleep@Pb"}
+print(f"block {os.environ.get('IPM_TRACE_BLOCK')} n={n}: {len(a)} workgroups, span {(a[:, 2].max() - t0) / 100:.1f} us")
+for r in sorted(set((a[:, 0] >> 32).tolist())):
+    s = a[(a[:, 0] >> 32) == r]
+    d = (s[:, 2] - s[:, 1]) / 100
+    print(f"  {names.get(r, r):14s} n={len(s):5d} start {(s[:, 1].min() - t0) / 100:7.1f}..{(s[:, 1].max() - t0) / 100:7.1f}"
+          f"  end {(s[:, 2].min() - t0) / 100:7.1f}..{(s[:, 2].max() - t0) / 100:7.1f}  dur mean {d.mean():6.1f} max {d.max():6.1f}")
+print(f"  distinct CU keys {len(set(a[:, 3].tolist()))}")

@@ -18,3 +18,6 @@ for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
 # first 12 blocks' events
 for r in rows[:40]:
     print(f"{(int(r['Start_Timestamp']) - t0) / 1e3:9.1f} {(int(r['End_Timestamp']) - t0) / 1e3:9.1f}  q{r.get('Queue_Id','?')} {r['Kernel_Name'][:50]}")
+print("... last blocks")
+for r in rows[-30:]:
+    print(f"{(int(r['Start_Timestamp']) - t0) / 1e3:9.1f} {(int(r['End_Timestamp']) - t0) / 1e3:9.1f}  q{r.get('Queue_Id','?')} {r['Kernel_Name'][:50]}")

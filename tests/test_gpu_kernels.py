@@ -47,7 +47,7 @@ def test_syrk_odd_ld_and_beta():
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * (1 + np.abs(X).max() ** 2 * k))
 
 
-@pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 513, 1030])
+@pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 300, 513, 640, 1030, 2100])
 def test_potrf_potrs_match_numpy(n):
     rng = np.random.default_rng(n)
     M = rng.normal(size=(n + 5, n))
@@ -63,12 +63,14 @@ def test_potrf_potrs_match_numpy(n):
     np.testing.assert_allclose(x, np.linalg.solve(A, b), rtol=1e-9, atol=1e-12)
 
 
-def test_potrf_reports_lapack_info():
-    n = 150
+# the failing column in the first panel, in a later block's first and second panels (the
+# failure must stop every later launch and come back as LAPACK's info)
+@pytest.mark.parametrize("n,bad", [(150, 97), (1030, 300), (1030, 450), (1030, 1029)])
+def test_potrf_reports_lapack_info(n, bad):
     rng = np.random.default_rng(0)
     M = rng.normal(size=(n, n))
     A = M @ M.T + np.eye(n)
-    A[97, 97] = -1e6        # leading minor 98 is not PD
+    A[bad, bad] = -1e6 * n   # leading minor bad+1 is not PD
     Hm = dev(A)
     rc, info = potrf(Hm, n, n)
     assert rc == 1

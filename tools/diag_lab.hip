@@ -15,14 +15,23 @@ int main() {
     hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice); hipMemset(info, 0, 4);
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     hipEventRecord(a);
-    hipMemset(ws + 2048 + 9216, 0, 64); hipLaunchKernelGGL(ipm::k_potrf_panel, dim3(1), dim3(256), 0, 0, (int64_t)128, (int64_t)0, 128, A, (int64_t)lda, ws, (unsigned*)(ws + 2048 + 9216), info);
+    hipMemset(ws + 2048 + 9216, 0, 64); hipLaunchKernelGGL(ipm::k_potrf_panel, dim3(1), dim3(256), 0, 0, (int64_t)128, (int64_t)0, 128, 0, A, (int64_t)lda, ws, (unsigned*)(ws + 2048 + 9216), info);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
-    unsigned long long st[64];
+    unsigned long long st[128];
     hipMemcpyFromSymbol(st, HIP_SYMBOL(ipm::ipm_stamps), sizeof(st));
-    printf("rep %d: %.1f us  stamps(cycles from start):", rep, ms * 1e3);
-    for (int i = 1; i < 27; ++i) printf(" %llu", st[i] - st[0]);
-    printf("\n");
+    printf("rep %d: %.1f us  load %llu cycles; per J: update / leaf+barrier / subst+barrier\n", rep, ms * 1e3,
+           st[1] - st[0]);
+    for (int J = 0; J < 8; ++J)
+      printf("  J=%d  %5llu %5llu %5llu   leaf end %5llu  inv end %5lld  pub end %5lld (from update end)\n", J,
+             st[2 + 3 * J] - st[1 + 3 * J], st[3 + 3 * J] - st[2 + 3 * J], st[4 + 3 * J] - st[3 + 3 * J],
+             st[32 + J] - st[2 + 3 * J], J ? (long long)(st[40 + J] - st[2 + 3 * J]) : 0LL,
+             J ? (long long)(st[48 + J] - st[2 + 3 * J]) : 0LL);
+    printf("  tail %llu  total %llu\n", st[26] - st[25], st[26] - st[0]);
+    for (int J = 1; J < 8; ++J)
+      printf("  J=%d wave1: writeback done %6lld, updates done %6lld | wave2: publish done %6lld, updates done %6lld\n", J,
+             (long long)(st[72 + J] - st[2 + 3 * J]), (long long)(st[88 + J] - st[2 + 3 * J]),
+             (long long)(st[80 + J] - st[2 + 3 * J]), (long long)(st[96 + J] - st[2 + 3 * J]));
   }
   return 0;
 }
