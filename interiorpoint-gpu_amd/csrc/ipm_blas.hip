@@ -1076,10 +1076,11 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
 static constexpr int64_t PANEL_WS = PF_DINV + 36 * 256;
 
-void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
   hipMemsetAsync(info, 0, sizeof(int), st);
-  if (n <= 0) return;
-  const int64_t nblocks = cdiv(n, CH_NB), cw = block_ctl_words(n);
+  if (ncols < 0 || ncols > n) ncols = n;
+  if (ncols <= 0) return;
+  const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
   // word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
   hipMemsetAsync(ctl0, 0, sizeof(unsigned) * (8 + nblocks * cw), st);
@@ -1094,7 +1095,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     b.wsB = ws + PANEL_WS;
     b.ctl = ctl0 + 8 + bk * cw;
     b.prevfail = bk == 0 ? ctl0 : ctl0 + 8 + (bk - 1) * cw + CTL_FAIL;
-    const int64_t cb = bk * CH_NB, wb = std::min<int64_t>(CH_NB, n - cb);
+    const int64_t cb = bk * CH_NB, wb = std::min<int64_t>(CH_NB, ncols - cb);
     b.cb = cb;
     b.wa = (int)std::min<int64_t>(wb, PF_NB);
     b.wbw = (int)(wb - b.wa);
@@ -1173,11 +1174,11 @@ static int panel_reserve_cus() {
 //                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
 // Without a side stream (side == main) the same sequence runs in order.
 void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
-                    double* ws) {
+                    double* ws, int64_t ncols) {
   // IPM_POTRF_LA=1: the earlier two-stream form below (kept for comparison); default: fused
   static const bool two_stream = [] { const char* e = getenv("IPM_POTRF_LA"); return e && e[0] == '1'; }();
   if (!two_stream) {
-    potrf_lower_fused(caller, n, A, lda, info, ws);
+    potrf_lower_fused(caller, n, A, lda, info, ws, ncols);
     return;
   }
   hipMemsetAsync(info, 0, sizeof(int), caller);

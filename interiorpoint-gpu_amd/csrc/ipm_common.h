@@ -64,19 +64,21 @@ inline int64_t potrf_ws_doubles(int64_t n) {
   return 2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8;
 }
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
-// one launch per 256-column block on stream s (the default behind potrf_lower / potrf_lower_la)
-void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
-// same with one block of look-ahead: panels on ps->side (high priority), trailing updates on
-// ps->main; both may be restricted to disjoint CU sets so the panel chain never waits for
-// trailing-update workgroups to drain.  ps == null or ps->side == null: everything in order on
-// `s`.  ps->main == null: trailing updates on `s` itself.  The call is ordered after earlier
-// work on `s`, and later work on `s` is ordered after it.
+// one launch per 256-column block on stream s (the default behind potrf_lower / potrf_lower_la).
+// ncols < n: only the first ncols columns are factored (all n rows) -- the bordered Newton system
+// needs row n-1 of L (the forward-solved right-hand side) but not its diagonal entry.
+void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws,
+                       int64_t ncols = -1);
+// default: potrf_lower_fused on s.  IPM_POTRF_LA=1: the earlier two-stream form -- panels on
+// ps->side (high priority), trailing updates on ps->main, events between them (ps == null or
+// ps->side == null: everything in order on s; ncols is ignored there).  The call is ordered
+// after earlier work on s, and later work on s is ordered after it.
 struct PotrfStreams {
   hipStream_t main = nullptr, side = nullptr;
   hipEvent_t ev_rel = nullptr, ev_pan = nullptr, ev_in = nullptr, ev_out = nullptr;
 };
 void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H, int64_t ldh, int* info_dev,
-                    double* ws);
+                    double* ws, int64_t ncols = -1);
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,

@@ -870,7 +870,8 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     ipm_handle* h = pr->h;
     border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws);
+    // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
+    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N);
     if (h->timing) hipEventRecord(h->ev[3], st);
     trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl);
   } else {
