@@ -660,12 +660,15 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 // starting step J as soon as the diagonal role has released block row J (*progress > J).
 // L blocks and Dinv come from the producer's sc1 stores and are read with sc1 loads only.
 // FUSED: as for diag_role; *done (if given) is set once this chunk's rows (and its part of the
-// next panel's columns) are stored.
+// next panel's columns) are stored.  next_nb > 0: the first nchd chunks publish their rows (the
+// next panel's diagonal block rows) and every chunk applies this panel to its rows of the next
+// panel's columns -- except the publishing chunks when fold_pub is false (the fused kernel folds
+// the next diagonal block with separate tile workgroups).
 template <bool FUSED = false>
 __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, int nb, double* __restrict__ A,
                                          int64_t lda, const double* dinv, const double* pubL,
                                          unsigned* progress, int next_nb, unsigned* nextc, double* stage,
-                                         int* sflag, unsigned* done = nullptr) {
+                                         int* sflag, unsigned* done = nullptr, bool fold_pub = true) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int64_t row = k0 + nb + chunk * PF_RB + wv * 16 + fr;
@@ -721,15 +724,15 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
         }
       }
   }
-  if (next_nb > 0) {
-  // ---- fused intra-block update (replaces a GEMM launch between the two panels of a block):
-  //   A[rows, k0+nb : k0+nb+next_nb] -= X[rows, :] L[k0+nb : k0+nb+next_nb, k0 : k0+nb]^T
-  // (nb == 128 here).  The second factor is this panel's result for the first nchd row chunks.
-  if (pub) {
+  if (next_nb > 0 && pub) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(nextc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (next_nb > 0 && (fold_pub || !pub)) {
+  // ---- fused intra-block update (replaces a GEMM launch between the two panels of a block):
+  //   A[rows, k0+nb : k0+nb+next_nb] -= X[rows, :] L[k0+nb : k0+nb+next_nb, k0 : k0+nb]^T
+  // (nb == 128 here).  The second factor is this panel's result for the first nchd row chunks.
   if (tid == 0) {
     int ok = 1;
     while (ld_ctl(nextc) < (unsigned)nchd) {
@@ -861,14 +864,18 @@ struct BlockArgs {
   int wa = 0, wbw = 0;
   int nla = 0, nra = 0, nrb = 0, la_tj = 0, nlab = 0;
   int64_t ns = 0;
+  int nnf = 0;                  // next-diagonal-block fold tiles (32 x 32, lower triangle)
   GemmArgs la, s;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
 };
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
-  CTL_PA_CU = 5, CTL_PB_CU = 6,   // 1 + CU key of the diagonal roles' workgroups
-  CTL_SPILL_A = 7, CTL_SPILL_B = 8,   // 1 + a trailing tile handed off by a workgroup on a diag CU
-  CTL_HDR = 16
+  CTL_NF = 9,                         // next-diagonal-block fold tiles done
+  // critical-path roles (P(a) diagonal, the row chunks P(b) needs, the NF tiles, P(b) diagonal):
+  // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
+  // by a workgroup that landed on that CU
+  CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
+  CTL_HDR = CTL_SPILL + NCRIT
 };
 
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
@@ -879,15 +886,6 @@ __device__ __forceinline__ unsigned cu_key() {
 }
 // control words per launch (block_ctl_words, ipm_common.h): header, la_done[ceil(n/64)],
 // pa_done[ceil(n/64)]
-
-// trailing tiles dispatched after the P(a) / P(b) row chunks (see the ticket order in k_potrf_block)
-#ifndef IPM_S_TAIL1
-#define IPM_S_TAIL1 0
-#endif
-#ifndef IPM_S_TAIL2
-#define IPM_S_TAIL2 0
-#endif
-constexpr int64_t S_TAIL1 = IPM_S_TAIL1, S_TAIL2 = IPM_S_TAIL2;
 
 union BlockSmem {
   DiagSmem d;
@@ -966,13 +964,13 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     wait_words(la_done + q0, (int)(q1 - q0 + 1), lat);
   };
   const int64_t k1 = b.cb + b.wa;
-  // ticket order after the LA tiles: P(a) diagonal, the P(a) row chunks P(b)'s diagonal block
-  // needs (nchd), P(b) diagonal, S tiles, the other P(a) row chunks, P(b) row chunks.  Row chunks
-  // spin while their diagonal role works; dispatched after the S tiles they do not hold slots
-  // the trailing update could use.  Decode first, then ONE call site per role (each role's code
+  // ticket order after the LA tiles: P(a) diagonal, the P(a) row chunks holding P(b)'s diagonal
+  // block rows (nchd), the tiles folding P(a) into that block (NF), P(b) diagonal, S tiles, the
+  // other P(a) row chunks, P(b) row chunks.  Row chunks spin while their diagonal role works;
+  // dispatched after the S tiles they do not hold slots the trailing update could use.  Decode first, then ONE call site per role (each role's code
   // is inlined once: register pressure and code size).
   const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-  enum { K_DIAG, K_ROW, K_TILE, K_NONE } kind = K_NONE;
+  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
   if (t == 0) {
@@ -980,45 +978,49 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   } else if ((t -= 1) < nchd) {
     kind = K_ROW;
     chunk = t;
+  } else if ((t -= nchd) < b.nnf) {
+    kind = K_NF;
   } else {
-    t -= nchd;
+    t -= b.nnf;
     if (b.wbw > 0 && t == 0) {
       kind = K_DIAG;
       pb = true;
     } else {
-      // [S seg 0][P(a) rows >= nchd][S seg 1][P(b) rows][S seg 2]: the row chunks are dispatched
-      // while the last tiles run (their diagonal roles are done by then) instead of after them
       if (b.wbw > 0) t -= 1;
-      const int64_t s2 = std::min<int64_t>(b.ns, S_TAIL2), s1 = std::min<int64_t>(b.ns - s2, S_TAIL1);
-      const int64_t s0 = b.ns - s1 - s2;
       const int64_t na = b.nra - nchd;
-      if (t < s0) {
+      if (t < b.ns) {
         kind = K_TILE;
-      } else if ((t -= s0) < na) {
+      } else if ((t -= b.ns) < na) {
         kind = K_ROW;
         chunk = nchd + t;
-      } else if ((t -= na) < s1) {
-        kind = K_TILE;
-        t += s0;
-      } else if ((t -= s1) < b.nrb) {
+      } else if ((t -= na) < b.nrb) {
         kind = K_ROW;
         pb = true;
         chunk = t;
-      } else if ((t -= b.nrb) < s2) {
-        kind = K_TILE;
-        t += s0 + s1;
       }
     }
   }
+  // critical-path role index (-1: none): keeps trailing tiles off this CU while it runs
+  int crit = -1;
+  if (kind == K_DIAG) crit = pb ? NCRIT - 1 : 0;
+  else if (kind == K_ROW && !pb && chunk < nchd) crit = 1 + (int)chunk;
+  else if (kind == K_NF) crit = 1 + nchd + (int)t;
+  if (crit >= NCRIT - 1 && !(kind == K_DIAG && pb)) crit = -1;   // (table full: not tracked)
+  if (crit >= 0 && tid == 0)
+    __hip_atomic_store(&b.ctl[CTL_CRIT + crit], 1u + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  struct CritEnd {   // clears the entry when the role returns
+    unsigned* w;
+    __device__ ~CritEnd() {
+      if (w && threadIdx.x == 0) __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } crit_end{crit >= 0 ? &b.ctl[CTL_CRIT + crit] : nullptr};
   double* ws = pb ? b.wsB : b.wsA;
   unsigned* prog = &b.ctl[pb ? CTL_PB_PROG : CTL_PA_PROG];
   const int64_t kp = pb ? k1 : b.cb;
   const int nbp = pb ? b.wbw : b.wa;
   if (kind == K_DIAG) {
     ROLE(pb ? 3 : 1);
-    if (tid == 0)
-      __hip_atomic_store(&b.ctl[pb ? CTL_PB_CU : CTL_PA_CU], 1u + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (pb) wait_words(pa_done, nchd, 1u);
+    if (pb) wait_words(&b.ctl[CTL_NF], 1, (unsigned)b.nnf);
     else wait_la(0, b.wa - 1);
     diag_role<true>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
     return;
@@ -1035,36 +1037,86 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       wait_la(r0, std::min<int64_t>(r0 + PF_RB, b.n - b.cb) - 1);
     }
     row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
-                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk]);
+                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk], false);
+    return;
+  }
+  if (kind == K_NF) {
+    ROLE(9);
+    // P(b)'s diagonal block -= L1D L1D^T, L1D = P(a)'s rows of that block (published by the first
+    // nchd row chunks): one 32 x 32 lower tile per workgroup, 16 x 16 per wave, K = wa = 128
+    int T = (b.wbw + 31) / 32, ti = 0, q = (int)t;
+    while (q > ti) { q -= ti + 1; ++ti; }   // t -> (ti, tj = q), tj <= ti
+    const int tj = q;
+    (void)T;
+    if (tid == 0) {
+      while (ld_ctl(&b.ctl[CTL_PA_NEXT]) < (unsigned)nchd && ld_ctl(&b.ctl[CTL_PA_PROG]) != 0xFFFFFFFFu)
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, fk = lane >> 4;
+    const int ib = 32 * ti + 16 * (wv & 1), jb = 32 * tj + 16 * (wv >> 1);
+    if (ib + 15 >= jb) {   // sub-tiles entirely above the diagonal are never read
+      const int i = ib + fr;
+      const bool iin = i < b.wbw;
+      dbl4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb + fk + 4 * r;
+        acc[r] = (iin && j < b.wbw) ? ld_sc1(&b.A[(k1 + j) * b.lda + k1 + i]) : 0.0;
+      }
+      const bool jin = jb + fr < b.wbw;
+      const double* pa = b.A + b.cb * b.lda + k1 + jb + fr;   // L1D[jb + fr][k] at pa[k * lda]
+      const double* pbp = b.A + b.cb * b.lda + k1 + i;        // L1D[i][k]
+      // all 64 operand loads in flight at once (one latency, not eight)
+      double av[32], bv[32];
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const int64_t k = 4 * q + fk;
+        av[q] = jin ? -ld_sc1(pa + k * b.lda) : 0.0;
+        bv[q] = iin ? ld_sc1(pbp + k * b.lda) : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);
+      if (iin) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = jb + fk + 4 * r;
+          if (j < b.wbw) st_sc1(&b.A[(k1 + j) * b.lda + k1 + i], acc[r]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&b.ctl[CTL_NF], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if (kind == K_TILE) {
     ROLE(4);
-    // A trailing tile that lands on the CU of a running diagonal role (the critical chain) hands
-    // its tile to the spill word of that role and sleeps, keeping the slot so that no MFMA tile
-    // shares the CU with the chain.  Every tile workgroup, after its own tile, takes what is in
-    // the spill words; the sleeper, once the role is done, runs its tile itself if nobody took it.
-    unsigned* spill[2] = {&b.ctl[CTL_SPILL_A], &b.ctl[CTL_SPILL_B]};
-    unsigned* dprog[2] = {&b.ctl[CTL_PA_PROG], &b.ctl[CTL_PB_PROG]};
+    // A trailing tile that lands on the CU of a running critical-path role hands its tile to
+    // that role's spill word and sleeps, keeping the slot so that no MFMA tile shares the CU with
+    // the chain.  Every tile workgroup, after its own tile, takes what is in the spill words; the
+    // sleeper, once the role is done, runs its tile itself if nobody took it.
     if (tid == 0) {
       const unsigned me = 1u + cu_key();
       int q = -1;
-      if (ld_ctl(&b.ctl[CTL_PA_CU]) == me && ld_ctl(dprog[0]) < 8u) q = 0;
-      else if (ld_ctl(&b.ctl[CTL_PB_CU]) == me && ld_ctl(dprog[1]) < 8u) q = 1;
+      for (int i = 0; i < NCRIT && q < 0; ++i)
+        if (ld_ctl(&b.ctl[CTL_CRIT + i]) == me) q = i;
       if (q >= 0) {
-        ROLE(7 + q);
-        __hip_atomic_store(spill[q], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (ld_ctl(dprog[q]) < 8u) __builtin_amdgcn_s_sleep(20);   // 0xFFFFFFFF (failure) ends it too
-        sflag = (int)__hip_atomic_exchange(spill[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ROLE(7);
+        __hip_atomic_store(&b.ctl[CTL_SPILL + q], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (ld_ctl(&b.ctl[CTL_CRIT + q]) == me) __builtin_amdgcn_s_sleep(20);
+        sflag = (int)__hip_atomic_exchange(&b.ctl[CTL_SPILL + q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         sflag = (int)(t + 1);
       }
     }
-    // own tile, then the two spill words (one tile call site: the tile code is inlined once)
+    // own tile, then the spill words (one tile call site: the tile code is inlined once)
 #pragma nounroll
-    for (int q = -1; q < 2; ++q) {
+    for (int q = -1; q < NCRIT; ++q) {
       if (q >= 0 && tid == 0)
-        sflag = (int)__hip_atomic_exchange(spill[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sflag = ld_ctl(&b.ctl[CTL_SPILL + q]) == 0u
+                    ? 0
+                    : (int)__hip_atomic_exchange(&b.ctl[CTL_SPILL + q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       const int v = sflag;
       __syncthreads();
@@ -1142,7 +1194,11 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
 #endif
     b.nra = (int)cdiv(std::max<int64_t>(n - cb - b.wa, 0), PF_RB);
     b.nrb = b.wbw > 0 ? (int)cdiv(std::max<int64_t>(n - cb - wb, 0), PF_RB) : 0;
-    const int64_t grid = b.nla + 1 + b.nra + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns;
+    {
+      const int T = (int)cdiv(b.wbw, 32);
+      b.nnf = T * (T + 1) / 2;
+    }
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns;
     if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
     else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
   }
