@@ -227,75 +227,75 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-// acc -= x[lane l of this 16-lane row] * x  (one v_fmac_f64 with a DPP row broadcast of src0;
+// acc -= xb[lane l of this 16-lane row] * x  (one v_fmac_f64 with a DPP row broadcast of src0;
 // gfx90a+ DPP64 supports row_newbcast).  l must fold to a constant.  nop: the first use of a
-// freshly written x carries the s_nop of the DPP read-after-VALU-write hazard in the same asm
+// freshly written xb carries the s_nop of the DPP read-after-VALU-write hazard in the same asm
 // statement (the compiler cannot move the producer between them).
-__device__ __forceinline__ void fmac_bcast16(double& acc, double x, int l, bool nop = false) {
+__device__ __forceinline__ void fmac_bcast16(double& acc, double xb, double x, int l, bool nop = false) {
   switch (l) {
     case 0:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 1:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 2:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 3:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 4:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 5:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:5 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 6:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:6 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 7:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:7 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 8:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 9:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:9 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 10:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:10 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 11:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:11 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 12:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:12 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 13:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:13 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 14:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:14 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
     case 15:
-      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %1 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
-      else asm volatile("v_fmac_f64_dpp %0, -%1, %1 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(x));
+      if (nop) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
+      else asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(xb), "v"(x));
       break;
   }
 }
@@ -351,7 +351,6 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
 // barrier that follows each block row's completion, thread 0 raises *progress (sc1).
 struct DiagSmem {
   double sD[36 * 256];   // L11 (identity-padded beyond nb)
-  double sLr[256];       // L_JJ row-major (broadcast reads of its rows)
   double srinv[8 * 16];  // 1 / L_cc per diagonal block
   int fail;
 };
@@ -364,7 +363,6 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
                                           double* pubL, unsigned* progress, DiagSmem& sm,
                                           unsigned* failw = nullptr) {
   double* sD = sm.sD;
-  double* sLr = sm.sLr;
   double* srinv = sm.srinv;
   int& fail = sm.fail;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 4 waves
@@ -477,12 +475,22 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   // final block column Jc of L11 -> A (lower part of the diagonal tile; i, j < nb); tiles
   // I = Jc + part, Jc + part + parts, ...
   auto write_back = [&](int Jc, int part, int parts) {
+    // lane: rows r2, r2+1 of columns c0 and c0+8 of each tile (16-byte stores when aligned)
+    const int r2 = 2 * (lane & 7), c0 = lane >> 3;
+    const bool v2 = ((lda & 1) == 0) && ((k0 & 1) == 0);
     for (int I = Jc + part; I < 8; I += parts) {
       const int cb = bidx(I, Jc) * 256;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = fk + 4 * q, i = I * 16 + fr, j = Jc * 16 + c;
-        if (i < nb && j < nb && (I > Jc || fr >= c)) A[(k0 + j) * lda + k0 + i] = sD[cb + c * 16 + fr];
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 8 * h, i = I * 16 + r2, j = Jc * 16 + c;
+        const double2 v = *reinterpret_cast<const double2*>(&sD[cb + c * 16 + r2]);
+        double* dst = A + (k0 + j) * lda + k0 + i;
+        if (v2 && I > Jc && i + 1 < nb && j < nb) {
+          *reinterpret_cast<double2*>(dst) = v;
+        } else if (j < nb) {
+          if (i < nb && (I > Jc || r2 >= c)) dst[0] = v.x;
+          if (i + 1 < nb && (I > Jc || r2 + 1 >= c)) dst[1] = v.y;
+        }
       }
     }
   };
@@ -491,36 +499,39 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   // tile; for the diagonal tile that is all the chain waits for); block column J+1 receives
   // terms 0..J-1 during the leaf of iteration J (waves 1-2, off the chain).
   for (int J = 0; J < 8; ++J) {
-    // ---- 1. term J-1 on block column J: wave 0 the diagonal tile (then straight on to factor
-    //      it), waves 1-3 the tiles below
-    if (J > 0)
+    // ---- 1. term J-1 on block column J: wave 0 the diagonal tile, waves 1-3 the tiles below
+    if (J > 0) {
       for (int tI = (wv == 0 ? 0 : wv); tI < 8 - J; tI += (wv == 0 ? 8 : 3)) tile_update(J + tI, J, J - 1);
+      __syncthreads();   // the leaf waves read tiles other waves updated
+    }
     STAMP();
-    // ---- 2. wave 0: factor the 16 x 16 block (J,J) in registers, lane r = row r.
-    //      Right-looking with NO lane masks: entries above the diagonal (lane r < column c)
-    //      turn into garbage but are never read -- every broadcast reads lane c2 > c or the
-    //      pivot lane.  sqrt and reciprocal come from one rsqrt (off one chain).
-    if (wv == 0) {
+    // ---- 2. factor the 16 x 16 block (J,J) in registers, lane r = row r (16-lane groups hold
+    //      copies), AND solve the tiles below it in the same sweep: lane group g of wave w holds
+    //      row r of tile (J+1+4w+g, J).  Right-looking, no lane masks: entries above the diagonal
+    //      turn into garbage but are never read -- every broadcast reads lane c2 > c or the pivot
+    //      lane.  The pivot chain is minimal: the next pivot is formed from two values read before
+    //      this column is scaled, l = A[c+1][c] dv_c, piv' = A[c+1][c+1] - l^2 (bitwise what the
+    //      vector update leaves in lane c+1), so dv_c -> dv_{c+1} is mul, fma, rsqrt; scaling and
+    //      rank-1 updates (one v_fmac_f64 with a DPP row broadcast of column c each) run beside it.
+    //      Wave 1 joins (a redundant copy of the chain) for the tiles wave 0 has no group for.
+    const int nbt = 7 - J;                                   // tiles below the diagonal one
+    const bool leafw = (wv == 0) || (wv == 1 && nbt > 4);
+    if (leafw) {
       const int db = bidx(J, J) * 256;
       const int rr = lane & 15;
-      double row[16];
+      const int Ib = J + 1 + 4 * wv + (lane >> 4);
+      const bool bval = Ib < 8;
+      const int bb = bidx(bval ? Ib : J, J) * 256;
+      double row[16], rowb[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = sD[db + c * 16 + rr];
-      // Column c+1 is updated first (readlane broadcast) and ITS pivot's rsqrt issued; the rest of
-      // column c's rank-1 update reads column c from an LDS copy (one write, a few wide reads
-      // instead of 2 readlanes per element) and fills the rsqrt latency.
+      for (int c = 0; c < 16; ++c) {
+        row[c] = sD[db + c * 16 + rr];
+        rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
+      }
       int bad = 0;
       double piv = readlane_d(row[0], 0);
       double dv = rsqrt_pivot(piv);
       double dvs[16];
-#ifndef IPM_LEAF
-#define IPM_LEAF 4
-#endif
-#if IPM_LEAF == 4
-      // pivot chain kept minimal: the next pivot is formed from two values read BEFORE this
-      // column is scaled, l = A[c+1][c] dv_c, piv' = A[c+1][c+1] - l^2 (bitwise what the vector
-      // update leaves in lane c+1), so dv_c -> dv_{c+1} is mul, fma, rsqrt; the column scaling
-      // and the rank-1 updates (one v_fmac_f64 with DPP row broadcast each) run beside it
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         if (!(piv > 0.0) && bad == 0) bad = c + 1;
@@ -534,64 +545,52 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
           dvn = rsqrt_pivot(pivn);
         }
         row[c] *= dv;                      // lane c: piv * dv = L_cc
+        rowb[c] *= dv;                     // X[r][c] of the tile below
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) fmac_bcast16(row[c2], row[c], c2, c2 == c + 1);
-        piv = pivn;
-        dv = dvn;
-      }
-#else
-      // column c's entries L[c2][c] go to scalar registers (v_readlane, all independent); the next
-      // column is updated and its pivot's rsqrt issued first, the other updates fill its latency
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        if (!(piv > 0.0) && bad == 0) bad = c + 1;
-        dvs[c] = dv;
-        row[c] *= dv;                      // lane c: piv * dv = L_cc
-        double l[16];
-#pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) l[c2] = readlane_d(row[c], c2);
-        double pivn = 1.0, dvn = 1.0;
-        if (c + 1 < 16) {
-          row[c + 1] = fma(-row[c], l[c + 1], row[c + 1]);
-          pivn = readlane_d(row[c + 1], c + 1);
-          dvn = rsqrt_pivot(pivn);
+        for (int c2 = c + 1; c2 < 16; ++c2) {
+          fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
+          fmac_bcast16(rowb[c2], row[c], rowb[c], c2, false);
         }
-#pragma unroll
-        for (int c2 = c + 2; c2 < 16; ++c2) row[c2] = fma(-row[c], l[c2], row[c2]);
         piv = pivn;
         dv = dvn;
       }
-#endif
-      if (lane < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (lane == c) srinv[J * 16 + c] = dvs[c];
-      }
-      if (lane < 16) {
+      if (bval) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
-          const double v = (rr >= c) ? row[c] : 0.0;
-          sD[db + c * 16 + rr] = v;          // column-major block
-          sLr[rr * 16 + c] = v;              // row-major copy
+          sD[bb + c * 16 + rr] = rowb[c];
+          if (pubL) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);
         }
       }
-      if (lane == 0 && bad) fail = J * 16 + bad;
+      if (wv == 0) {
+        if (lane < 16) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c)
+            if (lane == c) srinv[J * 16 + c] = dvs[c];
+#pragma unroll
+          for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = (rr >= c) ? row[c] : 0.0;   // column-major
+        }
+        if (lane == 0 && bad) fail = J * 16 + bad;
+      }
       STAMPAT(32 + J);
-    } else if (wv == 3 && J > 0) {
-      // meanwhile (off the chain) wave 3 inverts the PREVIOUS diagonal block for the row part
-      tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
-                    pubL != nullptr);
-      STAMPAT(40 + J);
     } else if (J > 0) {
-      // waves 1-2: wave 2 publishes the previous diagonal block; both apply terms 0..J-1 to the
-      // tiles of block column J+1 (look-ahead)
+      // the other waves, off the chain: wave 3 inverts the PREVIOUS diagonal block for the row
+      // part; wave 2 publishes it and writes block column J-1 back to A; the free waves apply
+      // terms 0..J-1 to the tiles of block column J+1 (look-ahead)
+      if (wv == 3) {
+        tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
+                      pubL != nullptr);
+        STAMPAT(40 + J);
+      }
       if (wv == 2 && pubL) {
         const int db = bidx(J - 1, J - 1) * 256;
 #pragma unroll
         for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
       }
+      if (wv >= 2) write_back(J - 1, wv - 2, 2);
       STAMPAT(64 + 8 * wv + J);
-      for (int I = J + wv; I < 8; I += 2) tile_update_n(I, J + 1, J);
+      // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin
+      const int f0 = nbt > 4 ? 2 : 1, nf = 4 - f0;
+      for (int I = J + 1 + (wv - f0); I < 8; I += nf) tile_update_n(I, J + 1, J);
       STAMPAT(80 + 8 * wv + J);
     }
     if (pubL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -600,30 +599,6 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     if (fail) break;
     // block row J-1 of L11 and Dinv_{J-1} are stored: release them to the row workgroups
     if (pubL && tid == 0 && J > 0) __hip_atomic_store(progress, (unsigned)J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // ---- 3. tiles below: X = T L_JJ^-T by substitution, one thread per tile row:
-    //      X[r][c] = (T[r][c] - sum_{k<c} X[r][k] L[c][k]) / L_cc
-    if (J > 0 && wv >= 2) write_back(J - 1, wv - 2, 2);   // (step 3 needs at most 112 threads)
-    if (tid < (7 - J) * 16) {
-      const int I = J + 1 + (tid >> 4), r = tid & 15;
-      const int cb = bidx(I, J) * 256 + r;
-      double x[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) x[c] = sD[cb + c * 16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        double v = x[c];
-#pragma unroll
-        for (int k = 0; k < c; ++k) v = fma(-x[k], sLr[c * 16 + k], v);
-        x[c] = v * srinv[J * 16 + c];
-      }
-#pragma unroll
-      for (int c = 0; c < 16; ++c) sD[cb + c * 16] = x[c];
-      if (pubL) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) st_sc1(&pubL[cb + c * 16], x[c]);
-      }
-    }
-    __syncthreads();
     STAMP();
   }
   if (fail) {

@@ -56,7 +56,7 @@ __global__ void k_leaf(double* io, unsigned long long* cyc, int reps) {
         }
         row[c] *= dv;
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) ipm::fmac_bcast16(row[c2], row[c], c2, c2 == c + 1);
+        for (int c2 = c + 1; c2 < 16; ++c2) ipm::fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
         piv = pivn;
         dv = dvn;
       }
@@ -77,7 +77,7 @@ __global__ void k_leaf(double* io, unsigned long long* cyc, int reps) {
       for (int c = 0; c < 16; ++c) {
         row[c] *= dv;
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) ipm::fmac_bcast16(row[c2], row[c], c2, c2 == c + 1);
+        for (int c2 = c + 1; c2 < 16; ++c2) ipm::fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
       }
     }
     for (int c = 0; c < 16; ++c) acc += dvs[c] + row[c];
