@@ -176,6 +176,11 @@ int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, int64_t ldx, 
 /* in-place Cholesky of the lower triangle of H (column-major, ldh); *info as LAPACK
    potrf (0 ok, j>0: leading minor j not positive definite).  work: [dev] >= 64 bytes */
 int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info);
+/* the first ncols columns only (0 <= ncols <= n): L11 = chol(H11) and L21 = H21 L11^-T, the
+   rows below ncols untouched otherwise.  The Newton step factors [[H, -g], [-g^T, .]] this way
+   with ncols = N, so row N becomes L^-1 (-g): the forward substitution of cho_solve
+   (NewtonSolver.py:303-313) rides inside the factorisation */
+int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double* H, int64_t ldh, int* info);
 /* solve L L^T X = B in place; L lower column-major (ldl); B row-major n x nrhs (ldb) */
 int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
               int64_t ldb);

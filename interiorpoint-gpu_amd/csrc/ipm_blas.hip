@@ -704,7 +704,13 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(nextc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (next_nb > 0 && (fold_pub || !pub)) {
+  // with fold_pub false a publishing chunk still folds its rows BELOW the next diagonal block
+  // (they exist when next_nb is not a multiple of PF_RB and rows follow it, e.g. the bordered
+  // right-hand-side row of the Newton factorization)
+  const int64_t nd_end = k0 + nb + next_nb;
+  const bool fold_chunk = fold_pub || !pub || (k0 + nb + (chunk + 1) * PF_RB > nd_end && nd_end < n);
+  const bool rfold = rin && (fold_pub || !pub || row >= nd_end);
+  if (next_nb > 0 && fold_chunk) {
   // ---- fused intra-block update (replaces a GEMM launch between the two panels of a block):
   //   A[rows, k0+nb : k0+nb+next_nb] -= X[rows, :] L[k0+nb : k0+nb+next_nb, k0 : k0+nb]^T
   // (nb == 128 here).  The second factor is this panel's result for the first nchd row chunks.
@@ -745,7 +751,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
       dbl4 acc;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        acc[r] = (rin && 16 * jt + fk + 4 * r < next_nb)
+        acc[r] = (rfold && 16 * jt + fk + 4 * r < next_nb)
                      ? (FUSED ? ld_sc1(&A[(col0 + fk + 4 * r) * lda + row]) : A[(col0 + fk + 4 * r) * lda + row])
                      : 0.0;
       const double* sb = stage + jl * SLAB + fk * 16 + fr;
@@ -754,7 +760,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
           acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-sb[(16 * P + 4 * s4) * 16], x[P][s4], acc, 0, 0, 0);
-      if (rin) {
+      if (rfold) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (16 * jt + fk + 4 * r < next_nb) {

@@ -511,7 +511,11 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
 }
 
 extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* info) {
-  if (!h || n < 0 || ldh < n) return IPM_INVALID_ARG;
+  return ipm_potrf_partial(h, n, n, H, ldh, info);
+}
+
+extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double* H, int64_t ldh, int* info) {
+  if (!h || n < 0 || ldh < n || ncols < 0 || ncols > n) return IPM_INVALID_ARG;
   if (n > h->pws_n) {
     if (h->pws) hipFree(h->pws);
     h->pws = nullptr;
@@ -519,7 +523,7 @@ extern "C" int ipm_potrf(ipm_handle* h, int64_t n, double* H, int64_t ldh, int* 
     HIPCHK(h, hipMalloc((void**)&h->pws, potrf_ws_doubles(n) * sizeof(double)));
     h->pws_n = n;
   }
-  potrf_lower_la(h->stream, &h->pst, n, H, ldh, h->dinfo, h->pws);
+  potrf_lower_la(h->stream, &h->pst, n, H, ldh, h->dinfo, h->pws, ncols);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;

@@ -6,7 +6,7 @@ OUT=gpurun_out/${TAG:-r1}
 mkdir -p $OUT
 make -j8 > $OUT/build.log 2>&1 || { echo "build failed"; tail -20 $OUT/build.log; exit 1; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 ${TT:-700} python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 ${TT:-700} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -15 $OUT/pytest_gpu.log
   [ $rc -ne 0 ] && exit $rc
 fi

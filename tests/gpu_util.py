@@ -37,11 +37,14 @@ def syrk(X, w, n, ldh=None, beta=0.0, H0=None, alpha=1.0):
     return H
 
 
-def potrf(Hmem, n, ldh):
+def potrf(Hmem, n, ldh, ncols=None):
     from ipm355 import _lib as L
     h = handle()
     info = ctypes.c_int(-7)
-    rc = h.lib.ipm_potrf(h.ptr, n, L.dptr(Hmem), ldh, ctypes.byref(info))
+    if ncols is None:
+        rc = h.lib.ipm_potrf(h.ptr, n, L.dptr(Hmem), ldh, ctypes.byref(info))
+    else:
+        rc = h.lib.ipm_potrf_partial(h.ptr, n, ncols, L.dptr(Hmem), ldh, ctypes.byref(info))
     return rc, info.value
 
 

@@ -47,6 +47,26 @@ def test_syrk_odd_ld_and_beta():
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * (1 + np.abs(X).max() ** 2 * k))
 
 
+@pytest.mark.parametrize("ncols,extra", [(128, 1), (129, 1), (200, 1), (200, 70), (255, 1), (256, 1), (257, 1),
+                                         (300, 1), (320, 64), (1000, 1), (2049, 1), (2048, 130)])
+def test_potrf_partial_bordered(ncols, extra):
+    """The bordered factorization of the Newton step: the first ncols columns are factored and
+    the rows below them (e.g. the -g row) get L21 = A21 L11^-T -- every block-size remainder,
+    including a next-panel diagonal block that ends inside a row chunk."""
+    n = ncols + extra
+    rng = np.random.default_rng(ncols * 7 + extra)
+    M = rng.normal(size=(n + 5, n))
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A.T.copy())
+    rc, info = potrf(Hm, n, n, ncols=ncols)
+    assert rc == 0 and info == 0
+    got = host(Hm).T                       # row-major view of the column-major buffer
+    L11 = np.linalg.cholesky(A[:ncols, :ncols])
+    L21 = np.linalg.solve(L11, A[ncols:, :ncols].T).T
+    np.testing.assert_allclose(np.tril(got[:ncols, :ncols]), L11, rtol=1e-10, atol=1e-10 * np.abs(L11).max())
+    np.testing.assert_allclose(got[ncols:, :ncols], L21, rtol=1e-10, atol=1e-10 * np.abs(L21).max())
+
+
 @pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 300, 513, 640, 1030, 2100])
 def test_potrf_potrs_match_numpy(n):
     rng = np.random.default_rng(n)
