@@ -189,6 +189,10 @@ int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t l
    averages (ms) over the Newton iterations since the reset, and their count */
 int ipm_set_timing(ipm_handle* h, int on);
 int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count);
+/* KKT-SYRK flops of one Newton step of this problem (m n (n+1) in total), split between the
+   up-front SYRK kernel and the k-row slices deferred into the Cholesky launches, where they fill
+   the CUs the panel chain leaves idle (opt-in, IPM_DEFER=1) */
+int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred);
 
 #ifdef __cplusplus
 }

@@ -11,10 +11,12 @@
 // (cuBLAS gemv/gemm via CuPy); NewtonSolver.py:286-313 (cuSOLVER potrf + 2 trsv);
 // NewtonSolverInfeasibleStart.py:398-452 (potrf + trsm with p right-hand sides).
 #include "ipm_common.h"
+#include <cstdio>
 #include "ipm_mfma.h"
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 #include <cstdlib>
 
 namespace ipm {
@@ -156,6 +158,44 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
   a.dvec = e.dvec;
   a.info = info;
   a.tri = 1;
+  if (e.kend_dev && e.kend_host) {
+    a.kend256 = e.kend_dev;
+    // variable work per tile: contiguous tile runs per XCD of equal work (tri order)
+    const int BM = 128;
+    const int64_t T = cdiv(n, BM), nt = T * (T + 1) / 2;
+    if (nt >= 768) {
+      std::vector<double> wt(nt);
+      double tot = 0;
+      for (int64_t L = 0; L < nt; ++L) {
+        int64_t bi = (int64_t)((std::sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+        while ((bi + 1) * (bi + 2) / 2 <= L) ++bi;
+        while (bi * (bi + 1) / 2 > L) --bi;
+        const int64_t bj = L - bi * (bi + 1) / 2, J = (bj * BM) >> 8;
+        const int64_t kt = std::min<int64_t>(k, J < e.nkend ? e.kend_host[J] : k);
+        wt[L] = (double)kt + 64.0;   // + epilogue (tP / H tile traffic) in k-row equivalents
+        tot += wt[L];
+      }
+      int64_t L = 0;
+      double acc = 0;
+      a.xb[0] = 0;
+      for (int x = 1; x < 8; ++x) {
+        while (L < nt && acc + 0.5 * wt[L] < tot * x / 8.0) acc += wt[L++];
+        a.xb[x] = (int)L;
+      }
+      a.xb[8] = (int)nt;
+      int maxc = 0;
+      for (int x = 0; x < 8; ++x) maxc = std::max(maxc, a.xb[x + 1] - a.xb[x]);
+      a.xbal = 1;
+      a.tiles_i = T;
+      a.nblk = nt;
+      const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
+                       ((((uintptr_t)a.Y) & 15) == 0);
+      dim3 g((unsigned)(8 * maxc)), b(256);
+      if (vec) hipLaunchKernelGGL((k_mfma_gemm<128, true, true>), g, b, 0, st, a);
+      else hipLaunchKernelGGL((k_mfma_gemm<128, true, false>), g, b, 0, st, a);
+      return;
+    }
+  }
   mfma_gemm_launch(st, a);
 }
 
@@ -846,6 +886,18 @@ struct BlockArgs {
   int nla = 0, nra = 0, nrb = 0, la_tj = 0, nlab = 0;
   int64_t ns = 0;
   int nnf = 0;                  // next-diagonal-block fold tiles (32 x 32, lower triangle)
+  // deferred KKT-SYRK slices run by this launch (DeferSyrk): job q = block column gs_J[q], slice
+  // gs_s[q] (first: G written, else accumulated), 64-tiles gs_cum[q] .. gs_cum[q+1]
+  static constexpr int MAXGS = 12;
+  int ngs = 0;
+  int gs_J[MAXGS] = {}, gs_s[MAXGS] = {}, gs_first[MAXGS] = {};
+  int64_t gs_cum[MAXGS + 1] = {};
+  int64_t gs_total = 0;          // == gs_cum[ngs]
+  const double* gX = nullptr;
+  const double* gw = nullptr;
+  double* G = nullptr;
+  int64_t gldx = 0, ldg = 0, gns = 0, gm = 0;
+  int gKS = 0;
   GemmArgs la, s;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
 };
@@ -930,7 +982,8 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   unsigned* pa_done = la_done + (b.n + 63) / 64;
   if (t < b.nla) {
     ROLE(0);
-    mfma_tile<64, false, VEC, 2, true>(b.la, t, sm.g64);
+    if (b.la.C2) mfma_tile<64, false, VEC, 2, true, true>(b.la, t, sm.g64);
+    else mfma_tile<64, false, VEC, 2, true>(b.la, t, sm.g64);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&la_done[t / b.la_tj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -951,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   // dispatched after the S tiles they do not hold slots the trailing update could use.  Decode first, then ONE call site per role (each role's code
   // is inlined once: register pressure and code size).
   const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_NONE } kind = K_NONE;
+  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_GS, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
   if (t == 0) {
@@ -978,6 +1031,8 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         kind = K_ROW;
         pb = true;
         chunk = t;
+      } else if ((t -= b.nrb) < b.gs_total) {
+        kind = K_GS;   // last: they fill the CUs the chain leaves idle
       }
     }
   }
@@ -1071,6 +1126,51 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     if (tid == 0) __hip_atomic_fetch_add(&b.ctl[CTL_NF], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  if (kind == K_GS) {
+    ROLE(10);
+    // never beside a critical-path role: wait (holding the slot) until none runs on this CU
+    if (tid == 0) {
+      const unsigned me = 1u + cu_key();
+      for (;;) {
+        bool busy = false;
+        for (int i = 0; i < NCRIT; ++i) busy |= ld_ctl(&b.ctl[CTL_CRIT + i]) == me;
+        if (!busy) break;
+        __builtin_amdgcn_s_sleep(20);
+      }
+    }
+    __syncthreads();
+    // G(:, block J) (+)= C_s^T diag(w_s) C_s over this job's k rows (64 x 64 tiles, rows >= 256 J)
+    // job lookup with constant indices only (a dynamically indexed kernel-argument array would
+    // put the whole argument block in scratch memory)
+    int gJ = 0, gsl = 0, gfirst = 0;
+    int64_t gbase = 0;
+#pragma unroll
+    for (int i = 0; i < BlockArgs::MAXGS; ++i)
+      if (i < b.ngs && t >= b.gs_cum[i]) {
+        gJ = b.gs_J[i];
+        gsl = b.gs_s[i];
+        gfirst = b.gs_first[i];
+        gbase = b.gs_cum[i];
+      }
+    const int64_t J0 = (int64_t)gJ * CH_NB, k0 = (int64_t)gsl * b.gKS;
+    GemmArgs g;
+    g.ni = b.gns - J0;
+    g.nj = std::min<int64_t>(CH_NB, b.gns - J0);
+    g.K = std::min<int64_t>(b.gKS, b.gm - k0);
+    g.X = g.Y = b.gX + k0 * b.gldx + J0;
+    g.ldx = g.ldy = b.gldx;
+    g.w = b.gw + k0;
+    g.C = b.G + J0 * b.ldg + J0;
+    g.ldc = b.ldg;
+    g.accum = gfirst ? 0 : 1;
+    g.rowmajor = 1;
+    g.xcd_remap = 0;
+    g.tiles_j = (g.nj + 63) / 64;
+    g.tiles_i = (g.ni + 63) / 64;
+    g.nblk = g.tiles_i * g.tiles_j;
+    mfma_tile<64, true, true, 2, false>(g, t - gbase, sm.g64);
+    return;
+  }
   if (kind == K_TILE) {
     ROLE(4);
     // A trailing tile that lands on the CU of a running critical-path role hands its tile to
@@ -1109,7 +1209,9 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
 static constexpr int64_t PANEL_WS = PF_DINV + 36 * 256;
 
-void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
+                       const DeferSyrk* ds) {
+  const bool defer = ds && ds->active();
   hipMemsetAsync(info, 0, sizeof(int), st);
   if (ncols < 0 || ncols > n) ncols = n;
   if (ncols <= 0) return;
@@ -1151,6 +1253,12 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       b.nla = (int)a.nblk;
       b.la_tj = (int)a.tiles_j;
       b.nlab = (int)a.tiles_i;
+      if (defer && bk < ds->nblocks && ds->d[bk] > 0 && cb < ds->ns) {
+        // block column bk's deferred KKT slices (G) join its look-ahead update
+        a.C2 = ds->G + cb * ds->ldg + cb;
+        a.ldc2 = ds->ldg;
+        a.n2 = ds->ns - cb;
+      }
       const int64_t m = n - cb - wb;
       if (m > 0) {
         GemmArgs& g = b.s;
@@ -1179,10 +1287,92 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
     }
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns;
+    if (defer) {
+      // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
+      b.gX = ds->X;
+      b.gldx = ds->ldx;
+      b.gw = ds->w;
+      b.G = ds->G;
+      b.ldg = ds->ldg;
+      b.gns = ds->ns;
+      b.gm = ds->m;
+      b.gKS = ds->KS;
+      for (int J = (int)bk + 1; J < ds->nblocks && J - 1 - bk < 64 && b.ngs < BlockArgs::MAXGS; ++J) {
+        const int dJ = ds->d[J];
+        const int off = J - 1 - (int)bk;             // bit of this launch in lm[J]
+        if (dJ <= 0 || !((ds->lm[J] >> off) & 1ull) || (int64_t)J * CH_NB >= ds->ns) continue;
+        const int q = b.ngs++;
+        const int step = off + 1 < 64 ? __builtin_popcountll(ds->lm[J] >> (off + 1)) : 0;   // earlier launches
+        b.gs_J[q] = J;
+        b.gs_s[q] = ds->nslices - dJ + step;
+        b.gs_first[q] = step == 0;
+        const int64_t ni = ds->ns - (int64_t)J * CH_NB, nj = std::min<int64_t>(CH_NB, ni);
+        b.gs_cum[q + 1] = b.gs_cum[q] + cdiv(ni, 64) * cdiv(nj, 64);
+      }
+      b.gs_total = b.gs_cum[b.ngs];
+    }
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns + b.gs_total;
     if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
     else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
   }
+}
+
+static int num_cus();
+static int num_cus_host() { return num_cus(); }
+// ---- deferred KKT slices: the plan.  A Cholesky launch lasts at least the panel chain of its
+// 256-column block (~115 us); CUs idle beyond what its look-ahead tiles, row chunks and trailing
+// tiles occupy can take slices.  Capacity model per launch L (units = one 64 x 64 x 256 tile,
+// ~25 us of one workgroup slot): 2 slots per CU over the chain time, minus LA tiles (1 unit),
+// trailing 128-tiles (3.6) and row chunks (3), times a fill factor.  Slices are assigned column
+// by column (ascending J, each to the latest launch < J with room: earliest deadline first).
+static double env_d(const char* k, double dflt) {
+  const char* e = getenv(k);
+  return e && *e ? atof(e) : dflt;
+}
+int defer_ks() {
+  const int ks = (int)env_d("IPM_DEFER_KS", 256);
+  return ks >= 16 ? ks : 256;
+}
+int defer_plan(int64_t ns, int64_t m, int KS, int nblocks, int* d, unsigned long long* lm) {
+  for (int J = 0; J < nblocks; ++J) { d[J] = 0; lm[J] = 0; }
+  // opt-in (IPM_DEFER=1): measured on MI355X at n=8192 the up-front SYRK shrinks by exactly what
+  // the Cholesky launches grow (2.80 -> 2.53 ms vs 6.80 -> 7.07 ms): the CUs the chain leaves idle
+  // are not free capacity
+  if (env_d("IPM_DEFER", 0) == 0 || m <= 0 || KS <= 0 || nblocks < 2) return 0;
+  const int nslices = (int)std::min<int64_t>((m + KS - 1) / KS, 63);
+  const int64_t N = (int64_t)nblocks * CH_NB;           // rows of the factored matrix (approx.)
+  const double fill = env_d("IPM_DEFER_FILL", 0.6), chain_us = env_d("IPM_DEFER_CHAIN_US", 115);
+  const double ucost = env_d("IPM_DEFER_UNIT_US", 25) * 256.0 / KS;   // one 64-tile slice task
+  const int slots = 2 * num_cus_host();
+  std::vector<double> cap(nblocks, 0.0);
+  std::vector<int> jobs(nblocks, 0);
+  for (int L = 1; L < nblocks; ++L) {
+    const int64_t cb = (int64_t)L * CH_NB, r = std::max<int64_t>(N - cb, 0);
+    const double la = 4.0 * ((r + 63) / 64), T = (double)((std::max<int64_t>(r - CH_NB, 0) + 127) / 128);
+    const double busy = la + 3.6 * T * (T + 1) / 2 + 3.0 * 2 * ((r + 63) / 64);
+    cap[L] = std::max(0.0, fill * (slots * chain_us / 25.0 - busy));
+  }
+  const int maxj = std::min((int)env_d("IPM_DEFER_MAXJOBS", BlockArgs::MAXGS), (int)BlockArgs::MAXGS);
+  int pairs = 0;
+  for (int J = 2; J < nblocks && (int64_t)J * CH_NB < ns; ++J) {
+    const int64_t rows = ns - (int64_t)J * CH_NB;
+    const double need = ((rows + 63) / 64) * ((std::min<int64_t>(rows, CH_NB) + 63) / 64) * ucost / 25.0;
+    for (int L = J - 1; L >= 1 && d[J] < nslices && L >= J - 63; --L) {
+      if (cap[L] >= need && jobs[L] < maxj) {
+        cap[L] -= need;
+        ++jobs[L];
+        ++d[J];
+        lm[J] |= 1ull << (J - 1 - L);
+        ++pairs;
+      }
+    }
+  }
+  if (env_d("IPM_DEFER_PRINT", 0) != 0) {
+    fprintf(stderr, "defer plan ns=%lld m=%lld KS=%d pairs=%d\n", (long long)ns, (long long)m, KS, pairs);
+    for (int J = 0; J < nblocks; ++J)
+      fprintf(stderr, "  J=%2d d=%d lm=%llx jobs(L=J)=%d cap_left=%.0f\n", J, d[J], lm[J], jobs[J], cap[J]);
+  }
+  return pairs;
 }
 
 static int num_cus() {
@@ -1211,11 +1401,11 @@ static int panel_reserve_cus() {
 //                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
 // Without a side stream (side == main) the same sequence runs in order.
 void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
-                    double* ws, int64_t ncols) {
+                    double* ws, int64_t ncols, const DeferSyrk* ds) {
   // IPM_POTRF_LA=1: the earlier two-stream form below (kept for comparison); default: fused
   static const bool two_stream = [] { const char* e = getenv("IPM_POTRF_LA"); return e && e[0] == '1'; }();
-  if (!two_stream) {
-    potrf_lower_fused(caller, n, A, lda, info, ws, ncols);
+  if (!two_stream || (ds && ds->active())) {
+    potrf_lower_fused(caller, n, A, lda, info, ws, ncols, ds);
     return;
   }
   hipMemsetAsync(info, 0, sizeof(int), caller);

@@ -108,6 +108,15 @@ struct ipm_problem {
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
   bool use_backup = false;
   bool pieces_valid = false;  // barrier pieces (inv/coef/G) match the current slack state
+  // KKT SYRK slices deferred into the Cholesky (DeferSyrk, ipm_common.h); LP/QP Cholesky path
+  std::vector<int> defer_d;   // per 256-column block; empty: no deferral
+  std::vector<unsigned long long> defer_lm;
+  std::vector<int> kend_h;
+  int64_t defer_pairs = 0;
+  int* kend_d = nullptr;
+  double* Gd = nullptr;
+  DeferSyrk dsy;
+  bool defer_on = false;
 };
 
 // ------------------------------------------------------------------------- workspace
@@ -153,6 +162,21 @@ void derive(ipm_problem* pr) {
   }
   // room for one bordered row (N+1 rows): the Newton right-hand side rides through the Cholesky
   pr->ldh = (pr->N + 1) + ((pr->N + 1) & 1);
+  // deferred KKT slices (sizes only; alignment is checked at problem creation)
+  pr->defer_d.clear();
+  pr->defer_lm.clear();
+  pr->defer_pairs = 0;
+  if (!pr->socp && pr->m > 0 && !pr->diag && !pr->lu) {
+    const int nb = (int)((pr->N + 255) / 256);
+    std::vector<int> dv(nb, 0);
+    std::vector<unsigned long long> lm(nb, 0);
+    const int64_t pairs = defer_plan(pr->n, pr->m, defer_ks(), nb, dv.data(), lm.data());
+    if (pairs > 0) {
+      pr->defer_d = dv;
+      pr->defer_lm = lm;
+      pr->defer_pairs = pairs;
+    }
+  }
 }
 
 int64_t carve(ipm_problem* pr, char* base) {
@@ -221,6 +245,11 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->part = c.take<double>(pe);
   pr->rowcone_d = c.take<int64_t>(pr->R + 1);
   pr->dslot_d = c.take<int64_t>(pr->K + 1);
+  if (!pr->defer_d.empty()) {
+    const int64_t ldg = n + (n & 1);
+    pr->Gd = c.take<double>(ldg * n);
+    pr->kend_d = c.take<int>((int64_t)pr->defer_d.size());
+  }
   return c.off + 256;
 }
 
@@ -342,7 +371,7 @@ void assemble_barrier_grad(ipm_problem* pr, double* B) {
 // Hessian into H (column-major lower, ldh) -- or the diagonal vector hdiag for the
 // diagonal strategy.  Requires barrier_pieces at the same slack state.
 // (FunctionManager.py:267-326, 547-611, 783-827, 1104-1158, 1372-1453)
-void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
+void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool defer = false) {
   const ipm_problem_desc& d = pr->d;
   hipStream_t st = S(pr);
   const double add = psd ? 1e-9 : 0.0;
@@ -364,6 +393,12 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
       if (pr->qp) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     }
     e.dvec = pr->dvec;
+    // defer: columns ahead stop at kend (their last slices run inside the Cholesky)
+    if (defer) {
+      e.kend_dev = pr->kend_d;
+      e.kend_host = pr->kend_h.data();
+      e.nkend = (int)pr->kend_h.size();
+    }
     syrk_lower(st, pr->n, pr->m, 1.0, d.C, d.ldc, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // border: hxs = -C^T inv_C^2 + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (+psd)
@@ -552,6 +587,28 @@ extern "C" int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms,
   return IPM_OK;
 }
 
+extern "C" int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred) {
+  // KKT SYRK flops (SYRK convention: 2 per multiply-add over the lower triangle incl. diagonal)
+  // split between the up-front SYRK kernel and the slices deferred into the Cholesky
+  if (!pr) return IPM_INVALID_ARG;
+  const double n = (double)pr->n;
+  const double m = (double)(pr->socp ? pr->XR : pr->m);
+  double def = 0.0;
+  if (pr->defer_on) {
+    const DeferSyrk& ds = pr->dsy;
+    for (int J = 0; J < ds.nblocks; ++J) {
+      const int64_t c0 = (int64_t)J * 256;
+      if (ds.d[J] <= 0 || c0 >= ds.ns) continue;
+      const double w = (double)std::min<int64_t>(256, ds.ns - c0), r = (double)(ds.ns - c0);
+      const double krows = (double)(ds.m - (int64_t)(ds.nslices - ds.d[J]) * ds.KS);
+      def += krows * (w * r - w * (w - 1) / 2.0) * 2.0;   // lower part of block column J
+    }
+  }
+  if (upfront) *upfront = m * n * (n + 1) - def;
+  if (deferred) *deferred = def;
+  return IPM_OK;
+}
+
 extern "C" int ipm_set_timing(ipm_handle* h, int on) {
   if (!h) return IPM_INVALID_ARG;
   h->timing = on != 0;
@@ -596,6 +653,29 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
   }
   carve(pr, reinterpret_cast<char*>(workspace));
   pr->use_backup = d.solve_method == IPM_SOLVE_LU;
+  if (!pr->defer_d.empty() && (d.ldc & 1) == 0 && (((uintptr_t)d.C) & 15) == 0) {
+    // deferred KKT slices: the up-front K extent per block, uploaded once
+    DeferSyrk& ds = pr->dsy;
+    ds.X = d.C;
+    ds.ldx = d.ldc;
+    ds.w = pr->w;
+    ds.m = pr->m;
+    ds.ns = pr->n;
+    ds.G = pr->Gd;
+    ds.ldg = pr->n + (pr->n & 1);
+    ds.KS = defer_ks();
+    ds.nslices = (int)((pr->m + ds.KS - 1) / ds.KS);
+    ds.nblocks = (int)pr->defer_d.size();
+    ds.d = pr->defer_d.data();
+    ds.lm = pr->defer_lm.data();
+    std::vector<int> kend(pr->defer_d.size());
+    for (size_t J = 0; J < kend.size(); ++J) kend[J] = (ds.nslices - pr->defer_d[J]) * ds.KS;
+    HIPCHK(h, hipMemcpyAsync(pr->kend_d, kend.data(), kend.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    pr->kend_h = kend;
+    ds.kend = pr->kend_d;
+    pr->defer_on = true;
+  }
   if (pr->socp) {
     // host-side structure: row -> cone, cone -> diagonal slot
     pr->rowcone_h.assign(pr->R + 1, 0);
@@ -867,7 +947,8 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     hipMemsetAsync(pr->info, 0, sizeof(int), st);
     return IPM_OK;
   }
-  assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
+  const bool defer = pr->defer_on && !pr->use_backup;
+  assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0, defer);
   if (!pr->use_backup) {
     // Cholesky of the bordered [[H, -g], [-g^T, big]]: its last row is y = L^-1 (-g) (the forward
     // solve of NewtonSolver.py:287-299 / cho_solve), then one backward solve L^T dx = y
@@ -875,7 +956,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
     // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
-    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N);
+    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
     if (h->timing) hipEventRecord(h->ev[3], st);
     trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl);
   } else {

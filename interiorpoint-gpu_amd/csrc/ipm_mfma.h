@@ -47,6 +47,12 @@ struct GemmArgs {
   int xcd_remap = 1;             // XCD-contiguous tile order (0: plain blockIdx order)
   int rowmajor = 0;              // tile L -> (L / tiles_j, L % tiles_j) (no remap): row blocks in order
   int64_t tiles_i = 0, tiles_j = 0, nblk = 0;
+  int accum = 0;                 // C += alpha-free sum (accumulators start from C, P/dvec ignored)
+  const int* kend256 = nullptr;  // per 256-column block of the tile's column: K extent (<= K)
+  const double* C2 = nullptr;    // sub/accum, FOLD instantiations: + C2(i, j) (i, j < n2) in the start value
+  int64_t ldc2 = 0, n2 = 0;
+  int xbal = 0;                  // blockIdx b -> tile xb[b % 8] + b / 8 (runs of equal work per XCD)
+  int xb[9] = {};
 };
 
 // agent-coherent (sc1) element access: data handed between workgroups of ONE launch
@@ -85,7 +91,9 @@ struct alignas(16) MfSmem {
 
 // One output tile (index Lw of the launch's tile space) by one workgroup of 128 * WJ threads.
 // SC1OUT: the tile is stored with sc1 stores (read by other workgroups of the same launch).
-template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false>
+// FOLD: a.C2 is folded into the start value (the Cholesky look-ahead tiles taking the deferred
+// KKT slices); a separate instantiation keeps the other tiles' register budget.
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
@@ -96,7 +104,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   {
     int64_t L = Lw;
     const int64_t q = a.nblk >> 3;
-    if (a.xcd_remap && !a.rowmajor && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
+    if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
     if (a.rowmajor) {
       bi = L / a.tiles_j;
       bj = L % a.tiles_j;
@@ -119,17 +127,22 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   const double* xp = a.X + sr * a.ldx + I0 + sc;
   const double* yp = a.Y + sr * a.ldy + J0 + sc;
   const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
-  const int64_t nslab = (a.K + BK - 1) / BK;
+  // K extent of this tile (the KKT SYRK with deferred slices: columns ahead take fewer k rows)
+  int kt32 = (int)a.K;
+  if (a.kend256) kt32 = __builtin_amdgcn_readfirstlane(std::min(kt32, a.kend256[J0 >> 8]));
+  const int64_t Kt = kt32;
+  const int64_t nslab = (Kt + BK - 1) / BK;
   // C -= X^T Y (Cholesky updates): the accumulators start FROM the C tile (its loads overlap the
-  // first slab's) and X is staged negated -- no dependent C read in the epilogue
-  const bool cinit = a.sub || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
-  const double xsg = cinit ? -1.0 : 1.0;
+  // first slab's) and X is staged negated -- no dependent C read in the epilogue.  accum: the
+  // same with C += X^T diag(w) Y (the deferred KKT slices).
+  const bool cinit = a.sub || a.accum || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
+  const double xsg = (cinit && !a.accum) ? -1.0 : 1.0;
   double rx[PT], ry[PT];
   auto gload = [&](int64_t s) {
     const int64_t k = s * BK + sr;
     const double* xs = xp + s * xstep;
     const double* ys = yp + s * ystep;
-    if (full && (s + 1) * BK <= a.K) {
+    if (full && (s + 1) * BK <= Kt) {
       const double wk = WEIGHT ? a.w[k] : 1.0;
       if (VEC) {
 #pragma unroll
@@ -149,7 +162,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
         }
       }
     } else {
-      const bool kin = k < a.K;
+      const bool kin = k < Kt;
       const double wk = (WEIGHT && kin) ? a.w[k] : 1.0;
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
@@ -181,7 +194,9 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
-          acc[tj][ti][r] = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
+          double v = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
+          if (FOLD && i < a.n2 && j < a.n2) v += a.C2[j * a.ldc2 + i];
+          acc[tj][ti][r] = v;
         }
       }
   }
@@ -247,6 +262,16 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
   __shared__ MfSmem<BM_, WJ> sm;
   __shared__ double spad[PAD > 0 ? PAD : 1];
   if (PAD > 0 && a.ni < 0) spad[threadIdx.x] = 0.0;   // never executed: keeps the pad allocated
+  if (a.xbal) {
+    // work-balanced XCD runs (constant-index selects: no dynamically indexed argument array)
+    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    int s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i == x) { s0 = a.xb[i]; s1 = a.xb[i + 1]; }
+    if (s0 + l < s1) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, s0 + l, sm);
+    return;
+  }
   for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
 }
 

@@ -160,6 +160,12 @@ class DeviceProblem:
         self.last_trace = [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
         return r
 
+    def kkt_flops(self):
+        """(up-front SYRK flops, flops of the slices deferred into the Cholesky) per Newton step"""
+        a, b = ct.c_double(), ct.c_double()
+        self.check(self.handle.lib.ipm_kkt_flops(self.ptr, ct.byref(a), ct.byref(b)))
+        return a.value, b.value
+
     @property
     def use_backup(self):
         return bool(self.handle.lib.ipm_get_use_backup(self.ptr))
