@@ -886,6 +886,7 @@ struct BlockArgs {
   int nla = 0, nra = 0, nrb = 0, la_tj = 0, nlab = 0;
   int64_t ns = 0;
   int nnf = 0;                  // next-diagonal-block fold tiles (32 x 32, lower triangle)
+  int s_map = 0;                // trailing-tile order (IPM_S_MAP)
   // deferred KKT-SYRK slices run by this launch (DeferSyrk): job q = block column gs_J[q], slice
   // gs_s[q] (first: G written, else accumulated), 64-tiles gs_cum[q] .. gs_cum[q+1]
   static constexpr int MAXGS = 12;
@@ -898,7 +899,8 @@ struct BlockArgs {
   double* G = nullptr;
   int64_t gldx = 0, ldg = 0, gns = 0, gm = 0;
   int gKS = 0;
-  GemmArgs la, s;
+  GemmArgs la32, la, s;          // look-ahead: 32-tiles (rows, cols < 128, lower), 64-tiles (rows >= 128)
+  int nla32 = 0, la32_T = 0;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
 };
 enum {
@@ -908,8 +910,26 @@ enum {
   // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
   // by a workgroup that landed on that CU
   CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
-  CTL_HDR = CTL_SPILL + NCRIT
+  CTL_XQ = CTL_SPILL + NCRIT,         // trailing-tile queue counter of each XCD (8 words)
+  CTL_HDR = CTL_XQ + 8
 };
+
+// Trailing tiles by XCD (s_map 2): the tri tile list is cut into 8 contiguous runs; a workgroup
+// takes the next tile of ITS XCD's run (HW_REG_XCC_ID); an exhausted run sends it on to the next
+// XCD's run.  One pass over the 8 runs always finds a tile (each tile-ticket takes exactly one
+// and runs are never refilled).  Returns the tile index in the tri enumeration.
+__device__ __forceinline__ int64_t xcd_tile(unsigned* xq, int64_t ntiles) {
+  const int64_t q = ntiles >> 3, rem = ntiles & 7;
+  const unsigned x0 = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // HW_REG_XCC_ID
+  for (unsigned d = 0; d < 8; ++d) {
+    const unsigned x = (x0 + d) & 7u;
+    const int64_t len = q + ((int64_t)x < rem ? 1 : 0), start = (int64_t)x * q + std::min<int64_t>(x, rem);
+    if ((int64_t)ld_ctl(&xq[x]) >= len) continue;
+    const int64_t i = (int64_t)atomicAdd(&xq[x], 1u);
+    if (i < len) return start + i;
+  }
+  return -1;   // unreachable (see above)
+}
 
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
 __device__ __forceinline__ unsigned cu_key() {
@@ -924,6 +944,7 @@ union BlockSmem {
   DiagSmem d;
   MfSmem<128, 2> g128;
   MfSmem<64, 2> g64;
+  MfSmem<32, 2> g32;
 };
 
 // thread 0 waits until words w[0..cnt) are all >= target; then the workgroup proceeds
@@ -980,22 +1001,46 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   }
   unsigned* la_done = b.ctl + CTL_HDR;
   unsigned* pa_done = la_done + (b.n + 63) / 64;
+  // look-ahead tiles: the first 128 rows x 128 columns (what the P(a) diagonal role waits for,
+  // lower part only) as 32 x 32 tiles -- ten short tiles instead of three 64-tiles on the chain --
+  // then 64-tiles for rows >= 128.  la_done[64-row block] counts finished tiles of that block.
   if (t < b.nla) {
     ROLE(0);
-    if (b.la.C2) mfma_tile<64, false, VEC, 2, true, true>(b.la, t, sm.g64);
-    else mfma_tile<64, false, VEC, 2, true>(b.la, t, sm.g64);
+    int64_t rb;
+    if (t < b.nla32) {
+      if (b.la32.C2) mfma_tile<32, false, VEC, 2, true, true>(b.la32, t, sm.g32);
+      else mfma_tile<32, false, VEC, 2, true>(b.la32, t, sm.g32);
+      int64_t i = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);   // tri row of tile t
+      while ((i + 1) * (i + 2) / 2 <= t) ++i;
+      while (i * (i + 1) / 2 > t) --i;
+      rb = i >> 1;
+    } else {
+      const int64_t t64 = t - b.nla32;
+      if (b.la.C2) mfma_tile<64, false, VEC, 2, true, true>(b.la, t64, sm.g64);
+      else mfma_tile<64, false, VEC, 2, true>(b.la, t64, sm.g64);
+      rb = 2 + t64 / b.la_tj;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&la_done[t / b.la_tj], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(&la_done[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   t -= b.nla;
-  const unsigned lat = (unsigned)b.la_tj;
   // LA row blocks [r0/64, r1/64] (rows relative to cb) finished
   auto wait_la = [&](int64_t r0, int64_t r1) {
     if (b.nla == 0) return;
     const int64_t q0 = r0 / 64, q1 = std::min<int64_t>(r1 / 64, b.nlab - 1);
-    wait_words(la_done + q0, (int)(q1 - q0 + 1), lat);
+    if (threadIdx.x == 0)
+      for (int64_t q = q0; q <= q1; ++q) {
+        // tiles per 64-row block: 32-tile tri rows 2q, 2q+1 (q < 2), else one row of 64-tiles
+        unsigned tgt = (unsigned)b.la_tj;
+        if (q < 2) {
+          tgt = 0;
+          for (int64_t i = 2 * q; i < 2 * q + 2 && i < b.la32_T; ++i) tgt += (unsigned)(i + 1);
+        }
+        while (ld_ctl(la_done + q) < tgt) __builtin_amdgcn_s_sleep(2);
+      }
+    __syncthreads();
   };
   const int64_t k1 = b.cb + b.wa;
   // ticket order after the LA tiles: P(a) diagonal, the P(a) row chunks holding P(b)'s diagonal
@@ -1178,6 +1223,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     // the chain.  Every tile workgroup, after its own tile, takes what is in the spill words; the
     // sleeper, once the role is done, runs its tile itself if nobody took it.
     if (tid == 0) {
+      if (b.s_map == 2) t = xcd_tile(&b.ctl[CTL_XQ], b.ns);   // this workgroup's tile: its XCD's run
       const unsigned me = 1u + cu_key();
       int q = -1;
       for (int i = 0; i < NCRIT && q < 0; ++i)
@@ -1236,13 +1282,33 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     b.wbw = (int)(wb - b.wa);
     if (bk > 0) {
       const int64_t cp = cb - CH_NB;
+      const int64_t ni = n - cb;
+      // rows [0, 128) x columns [0, min(128, wb)), lower: 32-tiles (tri enumeration)
+      GemmArgs& c = b.la32;
+      c.ni = std::min<int64_t>(ni, 128);
+      c.nj = std::min<int64_t>(c.ni, std::min<int64_t>(wb, 128));
+      c.ni = std::max(c.ni, c.nj);
+      c.K = CH_NB;
+      c.X = c.Y = A + cp * lda + cb;
+      c.ldx = c.ldy = lda;
+      c.C = A + cb * lda + cb;
+      c.ldc = lda;
+      c.sub = 1;
+      c.tri = 1;
+      c.xcd_remap = 0;
+      c.tiles_i = cdiv(c.ni, 32);
+      c.nblk = c.tiles_i * (c.tiles_i + 1) / 2;
+      b.nla32 = (int)c.nblk;
+      b.la32_T = (int)c.tiles_i;
+      // rows [128, ni) x all wb columns: 64-tiles, row blocks in order
       GemmArgs& a = b.la;
-      a.ni = n - cb;
+      a.ni = std::max<int64_t>(ni - 128, 0);
       a.nj = wb;
       a.K = CH_NB;
-      a.X = a.Y = A + cp * lda + cb;
+      a.X = A + cp * lda + cb + 128;
+      a.Y = A + cp * lda + cb;
       a.ldx = a.ldy = lda;
-      a.C = A + cb * lda + cb;
+      a.C = A + cb * lda + cb + 128;
       a.ldc = lda;
       a.sub = 1;
       a.rowmajor = 1;
@@ -1250,14 +1316,18 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       a.tiles_i = cdiv(a.ni, 64);
       a.tiles_j = cdiv(a.nj, 64);
       a.nblk = a.tiles_i * a.tiles_j;
-      b.nla = (int)a.nblk;
+      b.nla = b.nla32 + (int)a.nblk;
       b.la_tj = (int)a.tiles_j;
-      b.nlab = (int)a.tiles_i;
+      b.nlab = (int)cdiv(ni, 64);
       if (defer && bk < ds->nblocks && ds->d[bk] > 0 && cb < ds->ns) {
         // block column bk's deferred KKT slices (G) join its look-ahead update
-        a.C2 = ds->G + cb * ds->ldg + cb;
+        c.C2 = ds->G + cb * ds->ldg + cb;
+        c.ldc2 = ds->ldg;
+        c.n2 = c.n2c = ds->ns - cb;
+        a.C2 = ds->G + cb * ds->ldg + cb + 128;
         a.ldc2 = ds->ldg;
-        a.n2 = ds->ns - cb;
+        a.n2 = ds->ns - cb - 128;
+        a.n2c = ds->ns - cb;
       }
       const int64_t m = n - cb - wb;
       if (m > 0) {
@@ -1270,6 +1340,11 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         g.ldc = lda;
         g.sub = 1;
         g.tri = 1;
+        // trailing-tile order (IPM_S_MAP): 0 = XCD-remapped ticket order, 1 = plain tri order,
+        // 2 = per-XCD runs by HW_REG_XCC_ID
+        static const int smap = [] { const char* e = getenv("IPM_S_MAP"); return e ? atoi(e) : 0; }();
+        b.s_map = smap;
+        g.xcd_remap = smap == 0 ? 1 : 0;
         g.tiles_i = cdiv(m, 128);
         g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
         b.ns = g.nblk;

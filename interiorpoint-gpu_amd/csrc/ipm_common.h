@@ -64,7 +64,7 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
 // ws: device workspace of potrf_ws_doubles(n) doubles: two panels' inverted diagonal blocks and
 // published L11 blocks, then the control words (per launch: a header, one word per 64-row block
 // for the look-ahead tiles and one per 64-row chunk of the first panel)
-__host__ __device__ inline int64_t block_ctl_words(int64_t n) { return 48 + 2 * ((n + 63) / 64) + 8; }
+__host__ __device__ inline int64_t block_ctl_words(int64_t n) { return 56 + 2 * ((n + 63) / 64) + 8; }
 inline int64_t potrf_ws_doubles(int64_t n) {
   return 2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8;
 }

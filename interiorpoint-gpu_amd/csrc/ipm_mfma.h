@@ -50,7 +50,7 @@ struct GemmArgs {
   int accum = 0;                 // C += alpha-free sum (accumulators start from C, P/dvec ignored)
   const int* kend256 = nullptr;  // per 256-column block of the tile's column: K extent (<= K)
   const double* C2 = nullptr;    // sub/accum, FOLD instantiations: + C2(i, j) (i, j < n2) in the start value
-  int64_t ldc2 = 0, n2 = 0;
+  int64_t ldc2 = 0, n2 = 0, n2c = 0;   // C2 rows / columns (relative to the tile origin)
   int xbal = 0;                  // blockIdx b -> tile xb[b % 8] + b / 8 (runs of equal work per XCD)
   int xb[9] = {};
 };
@@ -195,7 +195,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
         for (int r = 0; r < 4; ++r) {
           const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
           double v = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
-          if (FOLD && i < a.n2 && j < a.n2) v += a.C2[j * a.ldc2 + i];
+          if (FOLD && i < a.n2 && j < a.n2c) v += a.C2[j * a.ldc2 + i];
           acc[tj][ti][r] = v;
         }
       }

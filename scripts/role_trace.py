@@ -32,3 +32,11 @@ for r in sorted(set((a[:, 0] >> 32).tolist())):
     print(f"  {names.get(r, r):14s} n={len(s):5d} start {(s[:, 1].min() - t0) / 100:7.1f}..{(s[:, 1].max() - t0) / 100:7.1f}"
           f"  end {(s[:, 2].min() - t0) / 100:7.1f}..{(s[:, 2].max() - t0) / 100:7.1f}  dur mean {d.mean():6.1f} max {d.max():6.1f}")
 print(f"  distinct CU keys {len(set(a[:, 3].tolist()))}")
+# S-tile durations by start time (are mid-launch tiles, with no panel work beside them, slower?)
+s = a[(a[:, 0] >> 32) == 4]
+st = (s[:, 1] - t0) / 100
+du = (s[:, 2] - s[:, 1]) / 100
+for lo in range(0, int(st.max()) + 50, 50):
+    m = (st >= lo) & (st < lo + 50)
+    if m.any():
+        print(f"    S tiles starting {lo:4d}-{lo + 50:4d} us: n={m.sum():4d} dur mean {du[m].mean():6.1f} min {du[m].min():6.1f}")

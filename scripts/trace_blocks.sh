@@ -1,4 +1,2 @@
 set -o pipefail
-for b in 1 4 8 12 16 20 24 28; do
-  IPM_TRACE_BLOCK=$b timeout -k 10 120 python scripts/role_trace.py 8192 || exit $?
-done
+for b in 1 6; do IPM_TRACE_BLOCK=$b timeout -k 10 120 python scripts/role_trace.py 8192 || exit $?; done
