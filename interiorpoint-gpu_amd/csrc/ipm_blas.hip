@@ -1847,6 +1847,243 @@ __global__ __launch_bounds__(256) void k_trsv_chain(int64_t n, int nblk, const d
   }
 }
 
+// -------------------------------------------------------------------------------------
+// Backward solve L^T x = b in 128-row blocks (the Newton step's second cho_solve half,
+// NewtonSolver.py:303-313; the first half rides inside the Cholesky as the bordered row).
+// Half the chain steps of the 64-row kernel, and each step is two small matrix-vector products
+// instead of a 64-step substitution: the owner of block B (ticket t = nblk-1-B, one workgroup of
+// 8 waves) computes, OFF the chain,
+//   * X_B = L_BB^-T (128 x 128, upper) by the panel kernels' 8-step MFMA block substitution
+//     X L_BB^T = I with inverted 16 x 16 diagonal blocks (wave w: rows 16w .. 16w+15),
+//   * pre = sum_{K >= B+2} L_KB^T x_K, streamed as those blocks are published,
+// and loads the tile L_{B+1,B} into registers.  The chain step is then
+//   rhs = b_B - pre - L_{B+1,B}^T x_{B+1};   x_B = X_B rhs
+// with thread (c, q) (c = column, q = quarter of the 128 k-indices) holding L_{B+1,B}[32q.., c]
+// in registers and X_B in LDS.  Hand-off as k_trsv_chain (sc1 stores, vmcnt(0), progress
+// word; consumers poll and read with sc1 loads).
+// -------------------------------------------------------------------------------------
+constexpr int TB2 = 128;
+// X_B = L_BB^-T for every 128-row diagonal block, one workgroup (8 waves) per block: the 8-step
+// MFMA block substitution X L_BB^T = I of the panel kernels' row role (wave w: rows 16w ..
+// 16w+15; X_J = 0 for J < w) with inverted 16 x 16 diagonal blocks.  Xws: nblk blocks of
+// 128 x 128, X[c][r] at c * 128 + r.  Identity beyond the last row.
+struct TrinvSmem {
+  double sD[36 * 256];
+  double sDinv[8 * 256];
+  double srinv[8 * 16];
+};
+__global__ __launch_bounds__(512, 1) void k_trinv128(int64_t n, const double* __restrict__ L, int64_t ldl,
+                                                     double* __restrict__ Xws) {
+  __shared__ TrinvSmem sm;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int B = blockIdx.x;
+  const int64_t r0 = (int64_t)B * TB2;
+  const int rows = (int)min((int64_t)TB2, n - r0);
+  for (int idx = tid; idx < 36 * 256; idx += 512) {
+    const int blk = idx >> 8, e = idx & 255, rr = e & 15, cc = e >> 4;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= blk) ++I;
+    const int J = blk - I * (I + 1) / 2;
+    const int i = I * 16 + rr, j = J * 16 + cc;
+    double v;
+    if (i < rows && j < rows) v = (i >= j) ? L[(r0 + j) * ldl + r0 + i] : 0.0;
+    else v = (i == j) ? 1.0 : 0.0;
+    sm.sD[idx] = v;
+  }
+  __syncthreads();
+  if (lane < 16) sm.srinv[wv * 16 + lane] = 1.0 / sm.sD[bidx(wv, wv) * 256 + lane * 16 + lane];
+  __syncthreads();
+  tri_inverse16(&sm.sD[bidx(wv, wv) * 256], &sm.srinv[wv * 16], &sm.sDinv[wv * 256], lane, false);
+  __syncthreads();
+  dbl4 x[8];
+#pragma unroll
+  for (int J = 0; J < 8; ++J) {
+    x[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+    if (J < wv) continue;
+    dbl4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = (J == wv && fr == fk + 4 * r) ? 1.0 : 0.0;   // identity block
+#pragma unroll
+    for (int P = 0; P < J; ++P) {
+      if (P < wv) continue;
+      const double* lb = &sm.sD[bidx(J, P) * 256 + fk * 16 + fr];
+      double av[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) av[s4] = -lb[64 * s4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], x[P][s4], acc, 0, 0, 0);
+    }
+    const double* ib = &sm.sDinv[J * 256 + fk * 16 + fr];
+    dbl4 xj = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(ib[64 * s4], acc[s4], xj, 0, 0, 0);
+    x[J] = xj;
+  }
+  // lane holds X[16w + fr][16J + fk + 4r]
+  double* xo = Xws + (int64_t)B * TB2 * TB2;
+#pragma unroll
+  for (int J = 0; J < 8; ++J)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xo[(16 * wv + fr) * TB2 + 16 * J + fk + 4 * r] = x[J][r];
+}
+
+// -------------------------------------------------------------------------------------
+// Backward solve L^T x = b in 128-row blocks (the Newton step's second cho_solve half,
+// NewtonSolver.py:303-313; the first half rides inside the Cholesky as the bordered row).
+// Half the chain steps of the 64-row kernel, and each step is two matrix-vector products
+// instead of a 64-step substitution.  The owner of block B (ticket t = nblk-1-B, one workgroup
+// of 8 waves) loads X_B = L_BB^-T (k_trinv128) into LDS, streams
+//   pre = sum_{K >= B+2} L_KB^T x_K
+// as those blocks are published, and holds the tile L_{B+1,B} in registers (thread (c, q): column
+// c, k-indices 32q .. 32q+31), all off the chain.  The chain step is then
+//   rhs = b_B - pre - L_{B+1,B}^T x_{B+1};   x_B = X_B rhs.
+// Hand-off as k_trsv_chain (sc1 stores, vmcnt(0), progress word; consumers poll and read with
+// sc1 loads).
+// -------------------------------------------------------------------------------------
+struct Trsv128Smem {
+  double sX[TB2 * (TB2 + 1)];   // X_B, X[c][r] at r * 129 + c
+  double sx[TB2];               // x_{B+1}
+  double sv[TB2];               // rhs
+  double spart[4][TB2];         // per-quarter partial sums
+  double spre[TB2];             // pre
+};
+
+__global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, const double* __restrict__ L,
+                                                        int64_t ldl, const double* __restrict__ b, int64_t bstride,
+                                                        const double* __restrict__ Xws, double* y, unsigned* ctl) {
+  __shared__ Trsv128Smem sm;
+  __shared__ int sticket;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 8 waves
+  const int c = tid & 127, q = tid >> 7;                          // critical layout
+  for (;;) {
+    if (tid == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
+    __syncthreads();
+    const int t = sticket;
+    __syncthreads();
+    if (t >= nblk) break;
+    const int B = nblk - 1 - t;
+    const int64_t r0 = (int64_t)B * TB2;
+    const int rows = (int)min((int64_t)TB2, n - r0);
+    {
+      const double* xs = Xws + (int64_t)B * TB2 * TB2;
+      for (int idx = tid; idx < TB2 * TB2; idx += 512) {
+        const int cc = idx >> 7, r = idx & 127;   // X[cc][r]
+        sm.sX[r * (TB2 + 1) + cc] = xs[idx];
+      }
+    }
+    const double bval = (q == 0 && c < rows) ? b[(r0 + c) * bstride] : 0.0;
+    // the tile L_{B+1,B} (rows of block B+1, columns of B): loaded first, it is needed right
+    // after the streaming below
+    double lt[32];
+    {
+      const int64_t k0 = r0 + TB2;
+      const int krows = (int)max((int64_t)0, min((int64_t)TB2, n - k0));
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        lt[k] = (B + 1 < nblk && c < rows && 32 * q + k < krows) ? L[(r0 + c) * ldl + k0 + 32 * q + k] : 0.0;
+    }
+    // ---- pre = sum_{K >= B+2} L_KB^T x_K in publication order; thread (lane, wave): rows
+    //      2 lane, 2 lane + 1 of each tile, columns 16 w .. 16 w + 15
+    double acc[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) acc[jj] = 0.0;
+    unsigned known = 0;
+#pragma nounroll
+    for (int tp = 0; tp + 1 < t; ++tp) {
+      const int64_t k0 = (int64_t)(nblk - 1 - tp) * TB2;
+      const int krows = (int)min((int64_t)TB2, n - k0);
+      const int kr = 2 * lane;
+      double tv0[16], tv1[16];
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) {
+        const int cc = 16 * wv + jj;
+        const double* src = L + (r0 + cc) * ldl + k0 + kr;
+        tv0[jj] = (cc < rows && kr < krows) ? src[0] : 0.0;
+        tv1[jj] = (cc < rows && kr + 1 < krows) ? src[1] : 0.0;
+      }
+      while (known <= (unsigned)tp) {
+        known = ld_ctl(&ctl[1]);
+        if (known <= (unsigned)tp) __builtin_amdgcn_s_sleep(1);
+      }
+      const double x0 = kr < krows ? ld_sc1(y + k0 + kr) : 0.0;
+      const double x1 = kr + 1 < krows ? ld_sc1(y + k0 + kr + 1) : 0.0;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) acc[jj] = fma(tv1[jj], x1, fma(tv0[jj], x0, acc[jj]));
+    }
+    // transpose-reduce the 16 column sums over the 64 lanes (17 shuffles): the halving steps over
+    // lane bits 5..2 leave each lane one column summed over 16 lanes
+    {
+      double v8[8], v4[4], v2[2], v1;
+      const bool u5 = lane & 32, u4 = lane & 16, u3 = lane & 8, u2 = lane & 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double snd = u5 ? acc[i] : acc[i + 8], kp = u5 ? acc[i + 8] : acc[i];
+        v8[i] = kp + __shfl_xor(snd, 32, 64);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double snd = u4 ? v8[i] : v8[i + 4], kp = u4 ? v8[i + 4] : v8[i];
+        v4[i] = kp + __shfl_xor(snd, 16, 64);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const double snd = u3 ? v4[i] : v4[i + 2], kp = u3 ? v4[i + 2] : v4[i];
+        v2[i] = kp + __shfl_xor(snd, 8, 64);
+      }
+      {
+        const double snd = u2 ? v2[0] : v2[1], kp = u2 ? v2[1] : v2[0];
+        v1 = kp + __shfl_xor(snd, 4, 64);
+      }
+      v1 += __shfl_xor(v1, 2, 64);
+      v1 += __shfl_xor(v1, 1, 64);
+      const int col = (u5 ? 8 : 0) + (u4 ? 4 : 0) + (u3 ? 2 : 0) + (u2 ? 1 : 0);
+      if ((lane & 3) == 0) sm.spre[16 * wv + col] = v1;
+    }
+    __syncthreads();
+    // ---- the chain step
+    if (t > 0) {
+      const int64_t k0 = r0 + TB2;
+      const int krows = (int)min((int64_t)TB2, n - k0);
+      if (tid == 0)
+        while (ld_ctl(&ctl[1]) < (unsigned)t) __builtin_amdgcn_s_sleep(1);
+      __syncthreads();
+      if (tid < TB2) sm.sx[tid] = tid < krows ? ld_sc1(y + k0 + tid) : 0.0;
+      __syncthreads();
+      double p = 0.0, p2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 32; k += 2) {
+        p = fma(lt[k], sm.sx[32 * q + k], p);
+        p2 = fma(lt[k + 1], sm.sx[32 * q + k + 1], p2);
+      }
+      sm.spart[q][c] = p + p2;
+    } else {
+      sm.spart[q][c] = 0.0;
+    }
+    __syncthreads();
+    if (q == 0) sm.sv[c] = bval - sm.spre[c] - ((sm.spart[0][c] + sm.spart[1][c]) + (sm.spart[2][c] + sm.spart[3][c]));
+    __syncthreads();
+    {
+      double p = 0.0, p2 = 0.0;
+      const double* xc = &sm.sX[32 * q * (TB2 + 1) + c];   // X[c][32q + k] at xc[k * 129]
+#pragma unroll
+      for (int k = 0; k < 32; k += 2) {
+        p = fma(xc[k * (TB2 + 1)], sm.sv[32 * q + k], p);
+        p2 = fma(xc[(k + 1) * (TB2 + 1)], sm.sv[32 * q + k + 1], p2);
+      }
+      __syncthreads();
+      sm.spart[q][c] = p + p2;
+    }
+    __syncthreads();
+    if (q == 0 && c < rows)
+      st_sc1(y + r0 + c, (sm.spart[0][c] + sm.spart[1][c]) + (sm.spart[2][c] + sm.spart[3][c]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&ctl[1], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+  }
+}
+
 static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int64_t ldl, const double* b,
                        int64_t bstride, double* y, unsigned* ctl) {
   const int nblk = (int)cdiv(n, TV_B);
@@ -1859,10 +2096,19 @@ static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int
 
 // L^T x = b (b read with stride bstride, e.g. the bordered row of a Cholesky factor); ctl: 2 words
 void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
-                  double* x, unsigned* ctl) {
+                  double* x, unsigned* ctl, double* xinv_ws) {
   if (n <= 0) return;
   hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned), st);
-  trsv_chain(st, false, n, L, ldl, b, bstride, x, ctl);
+  // without the inverse workspace (or IPM_TRSV64=1): the 64-row substitution kernel
+  static const bool k64 = [] { const char* e = getenv("IPM_TRSV64"); return e && e[0] == '1'; }();
+  if (k64 || !xinv_ws) {
+    trsv_chain(st, false, n, L, ldl, b, bstride, x, ctl);
+    return;
+  }
+  const int nblk = (int)cdiv(n, TB2);
+  hipLaunchKernelGGL(k_trinv128, dim3(nblk), dim3(512), 0, st, n, L, ldl, xinv_ws);
+  const int grid = std::min(nblk, 256);
+  hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl);
 }
 
 // Bordered right-hand side: row N of the (N+1) x (N+1) column-major lower factor input holds
@@ -1880,12 +2126,12 @@ void border_rhs(hipStream_t st, int64_t N, double* H, int64_t ldh, const double*
 // L L^T X = B in place; W: scratch n x nrhs (ldb); ctl: device scratch of 4 words (single
 // right-hand side only; may be null, then the blocked multi-RHS path is used)
 void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W, unsigned* ctl) {
+                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws) {
   if (n <= 0 || nrhs <= 0) return;
   if (nrhs == 1 && ldb == 1 && ctl) {
     hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned), st);
     trsv_chain(st, true, n, L, ldl, B, 1, W, ctl);
-    trsv_chain(st, false, n, L, ldl, W, 1, B, ctl + 2);
+    trsv_lower_t(st, n, L, ldl, W, 1, B, ctl + 2, xinv_ws);
     return;
   }
   trsm_lower_fwd(st, n, nrhs, L, ldl, B, ldb, W);

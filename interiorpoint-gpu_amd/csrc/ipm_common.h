@@ -112,10 +112,13 @@ void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H,
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W, unsigned* ctl);
+                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws = nullptr);
 // L^T x = b, one right-hand side read with stride bstride; ctl: 2 device words
+// xinv_ws: trsv_inv_ws_doubles(n) doubles for the inverted 128 x 128 diagonal blocks (null: the
+// 64-row substitution kernel)
 void trsv_lower_t(hipStream_t s, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
-                  double* x, unsigned* ctl);
+                  double* x, unsigned* ctl, double* xinv_ws = nullptr);
+inline int64_t trsv_inv_ws_doubles(int64_t n) { return ((n + 127) / 128) * 128 * 128; }
 // H[j*ldh + N] = scale * g[j] (j < N), H[N*ldh + N] = 1e300: bordered right-hand side (see ipm_blas.hip)
 void border_rhs(hipStream_t s, int64_t N, double* H, int64_t ldh, const double* g, double scale);
 // forward L Y = B / backward L^T Y = B: B is consumed, the solution goes to Y (same ld)

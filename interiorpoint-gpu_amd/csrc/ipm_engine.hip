@@ -103,6 +103,7 @@ struct ipm_problem {
   int* info = nullptr;
   unsigned* ctl = nullptr;  // persistent-solve control words
   double* pws = nullptr;    // Cholesky panel workspace (inverted diagonal blocks)
+  double* xinv = nullptr;   // backward solve: inverted 128 x 128 diagonal blocks of L
   int64_t part_elems = 0, nls_blocks = 0;
   std::vector<int64_t> rowcone_h, dslot_h;
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
@@ -224,6 +225,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->pmask = c.take<unsigned long long>(nls + 1);
   pr->psum = c.take<double>((nls + 1) * NCAND);
   pr->H = c.take<double>(pr->ldh * (N + 1));
+  pr->xinv = c.take<double>(trsv_inv_ws_doubles(N));
   pr->W2 = c.take<double>(N * std::max<int64_t>(p, 1));
   pr->piv = c.take<int64_t>(N);
   if (pr->eq) {
@@ -570,9 +572,10 @@ extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double
 extern "C" int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                          int64_t ldb) {
   if (!h || n < 0 || nrhs < 0 || ldl < n || ldb < nrhs) return IPM_INVALID_ARG;
-  double* W = scratch(h, std::max<int64_t>(n * ldb, 1) * sizeof(double));
+  const int64_t wn = (std::max<int64_t>(n * ldb, 1) + 31) & ~int64_t(31);
+  double* W = scratch(h, (wn + trsv_inv_ws_doubles(n)) * sizeof(double));
   if (!W) return IPM_HIP_ERROR;
-  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W, h->ctl);
+  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W, h->ctl, W + wn);
   HIPCHK(h, hipGetLastError());
   return IPM_OK;
 }
@@ -958,7 +961,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
     potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
     if (h->timing) hipEventRecord(h->ev[3], st);
-    trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl);
+    trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv);
   } else {
     lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
@@ -1009,7 +1012,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     copy(st, pr->Ybuf, d.AT, n * p);
     potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
     copy(st, pr->tmpn, pr->g, n);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl, pr->xinv);
     // S = A Y (lower)
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
@@ -1021,7 +1024,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     // dx = -H^-1 (g + A^T w)
     gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
     lincomb(st, n, -1.0, pr->g, -1.0, pr->ATdv, pr->dx);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl, pr->xinv);
     lincomb(st, p, 1.0, pr->wv, -1.0, v, pr->dv);
     return IPM_OK;
   }
