@@ -34,18 +34,34 @@ import numpy as np  # noqa: E402
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (256 CU x 2.4 GHz x 128)
 HBM_PEAK_GBS = 8000.0
-# HBM bytes per KKT-SYRK launch from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate
-# passes, FETCH doubled per MI355X_MICROARCH.md) of this same bench: scripts/pmc_summary.py
-PMC_FILE = os.path.join(REPO, "profiles", "pmc_kkt_syrk.json")
+# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate passes,
+# FETCH doubled per MI355X_MICROARCH.md) of this same bench: scripts/pmc_summary.py
+PMC_SYRK = os.path.join(REPO, "profiles", "pmc_kkt_syrk.json")
+PMC_POTRF = os.path.join(REPO, "profiles", "pmc_potrf_block.json")
 
 
-def pmc_traffic(n, m):
-    """PMC-measured HBM bytes per KKT-SYRK launch, only if the committed profile is of this (n, m)."""
+def pmc_traffic(path, n, m):
+    """PMC-measured HBM bytes per launch, only if the committed profile is of this (n, m)."""
     try:
-        d = json.load(open(PMC_FILE))
+        d = json.load(open(path))
         return float(d["hbm_bytes_per_launch"]) if (d.get("n"), d.get("m")) == (n, m) else None
     except Exception:
         return None
+
+
+def trailing_bytes(N, nb=256):
+    """HBM bytes of a right-looking blocked Cholesky: the lower trailing matrix read + written once
+    per block (16 B per element)."""
+    tot = 0.0
+    for b0 in range(0, N, nb):
+        r = N - b0
+        tot += 16.0 * r * (r + 1) / 2
+    return tot
+
+
+def potrf_flops(N):
+    """Cholesky of the N x N Newton matrix (the bordered right-hand side row adds O(N^2))."""
+    return N ** 3 / 3 + N ** 2 / 2 + N / 6
 
 
 def make_instance(n, m, seed, dev):
@@ -175,10 +191,11 @@ def main():
     a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     h.lib.ipm_last_timings(h.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
     kkt_ms, potrf_ms, cnt = a.value, b.value, c.value
-    done = sum(sum(s.phase1_solver.inner_iters) + sum(s.inner_iters) for s in solvers)
+    p1 = sum(sum(s.phase1_solver.inner_iters) for s in solvers)
+    done = p1 + sum(sum(s.inner_iters) for s in solvers)
     inst = insts[0]
 
-    stats = torch.tensor([el, float(done), kkt_ms, potrf_ms], dtype=torch.float64, device=dev)
+    stats = torch.tensor([el, float(done), kkt_ms, potrf_ms, float(p1)], dtype=torch.float64, device=dev)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)          # the only collective: end-of-run gather over xGMI
@@ -190,10 +207,13 @@ def main():
         total_iters = float(allst[:, 1].sum())
         n, m = args.n, args.m
         syrk_flops = m * n * (n + 1) + n * n      # Cholesky-KKT assembly: SYRK + tP epilogue
-        potrf_flops = n ** 3 / 3 + n ** 2 / 2 + n / 6
+        # phase-1 iterations factor the (n+1)-variable system, the others n (rank 0's mix)
+        f1 = float(allst[0, 4]) / max(float(allst[0, 1]), 1.0)
+        pf = f1 * potrf_flops(n + 1) + (1 - f1) * potrf_flops(n)
+        launches = f1 * ((n + 1 + 255) // 256) + (1 - f1) * ((n + 255) // 256)   # one per 256 columns
         kkt_tf = syrk_flops / (float(allst[0, 2]) * 1e-3) / 1e12 if allst[0, 2] > 0 else 0.0
-        potrf_tf = potrf_flops / (float(allst[0, 3]) * 1e-3) / 1e12 if allst[0, 3] > 0 else 0.0
-        f_iter = m * n * (n + 1) + potrf_flops + 2 * n * n
+        potrf_tf = pf / (float(allst[0, 3]) * 1e-3) / 1e12 if allst[0, 3] > 0 else 0.0
+        f_iter = m * n * (n + 1) + pf + 2 * n * n
         value = total_iters / tmax
         rec = {
             "metric": "Newton iters/sec, dense QP n=8192, 1/2/4/8 GPUs; achieved % fp64 roofline",
@@ -206,12 +226,22 @@ def main():
                                    + (" solved concurrently (one stream + host thread each)" if args.concurrent else ""),
                        "n": n, "m": m, "instances_per_gpu": args.instances,
                        "parallelism": f"instances{world * args.instances}"},
-            "roofline": {"bound": "mfma", "achieved": kkt_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(n, m),
-                         "kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = tP + C^T diag(w) C + diag)",
+            # dominant kernel: the Cholesky, one k_potrf_block launch per 256 columns; achieved =
+            # factorization flops / HIP-event time of all its launches (= per-launch flops / avg launch)
+            "roofline": {"bound": "mfma", "achieved": potrf_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": potrf_tf / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(PMC_POTRF, n, m),
+                         "kernel": "k_potrf_block (blocked Cholesky of the Newton matrix, bordered RHS row)",
+                         "flops_per_launch": pf / launches, "avg_launch_ms": float(allst[0, 3]) / launches,
+                         "launches_per_factorization": launches,
+                         # right-looking blocked Cholesky: each launch reads and writes the lower
+                         # trailing matrix once (16 B per element), averaged over the launches
+                         "algorithmic_bytes_per_launch": trailing_bytes(n + 1 if f1 >= 0.5 else n) / launches},
+            "kkt_syrk": {"kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = tP + C^T diag(w) C + diag)",
+                         "achieved_tflops": kkt_tf, "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS,
                          "flops_per_launch": syrk_flops, "avg_launch_ms": float(allst[0, 2]),
+                         "traffic": pmc_traffic(PMC_SYRK, n, m),
                          "algorithmic_bytes_per_launch": 8 * (m * n + m + n * (n + 1) / 2 * 2)},
-            "potrf": {"achieved_tflops": potrf_tf, "avg_ms": float(allst[0, 3]), "flops": potrf_flops},
+            "potrf": {"achieved_tflops": potrf_tf, "avg_ms": float(allst[0, 3]), "flops": pf},
             "whole_iteration_fp64_frac": (f_iter * total_iters / world / tmax) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "newton_iters": total_iters,
         }

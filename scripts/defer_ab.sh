@@ -13,5 +13,5 @@ for cfg in ${CFGS:-"IPM_DEFER=0" "IPM_DEFER=1" "IPM_DEFER_FILL=1" "IPM_DEFER_FIL
   [ $rc -ne 0 ] && { echo "$cfg bench rc=$rc"; tail -5 gpurun_out/defer/b.err; exit $rc; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/defer/b.json').read().strip().splitlines()[-1])
-print('$cfg', round(d['value'],2), 'kkt', round(d['roofline']['avg_launch_ms'],3), 'potrf', round(d['potrf']['avg_ms'],3))"
+print('$cfg', round(d['value'],2), 'kkt', round(d['kkt_syrk']['avg_launch_ms'],3), 'potrf', round(d['potrf']['avg_ms'],3))"
 done
