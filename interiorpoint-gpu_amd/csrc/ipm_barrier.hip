@@ -405,29 +405,45 @@ __device__ __forceinline__ void lane_reduce_store(double (&vals)[64], unsigned l
   if (threadIdx.x == 0) pmask[blockIdx.x] = ((mred[0] & mred[1]) & mred[2]) & mred[3];
 }
 
+// 64 slacks per workgroup; wave w evaluates candidates 16w .. 16w+15 for all 64 (lane = slack),
+// so a wave sum is a candidate's partial and no cross-wave reduction is needed.  4x the
+// workgroups of a one-slack-per-thread form (the 64 logs per slack were the cost).
+constexpr int LS_EPB = 64;   // slacks per workgroup
 __global__ __launch_bounds__(256) void k_ls_lin(int64_t len, int64_t bar_len, const double* __restrict__ s0,
                                                 const double* __restrict__ ds, double alpha0, double beta,
                                                 unsigned long long* __restrict__ pmask,
                                                 double* __restrict__ psum) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double vals[64];
-  unsigned long long mask = ~0ull;
+  __shared__ unsigned long long mq[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * LS_EPB + lane;
+  double a = alpha0;
+  for (int q = 0; q < 16 * wv; ++q) a = a * beta;   // alpha_{16w}, as the host table forms it
+  double vals[16];
+  unsigned mask = 0xFFFFu;
   if (e < len) {
     const double a0 = s0[e], d = ds[e];
     const bool bar = e < bar_len;
-    double a = alpha0;
 #pragma unroll
-    for (int k = 0; k < 64; ++k) {
+    for (int k = 0; k < 16; ++k) {
       const double v = a0 + a * d;
-      if (v < 0.0) mask &= ~(1ull << k);
+      if (v < 0.0) mask &= ~(1u << k);
       vals[k] = bar ? log(v + EPS_LOG) : 0.0;
       a = a * beta;
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < 64; ++k) vals[k] = 0.0;
+    for (int k = 0; k < 16; ++k) vals[k] = 0.0;
   }
-  lane_reduce_store(vals, mask, pmask, psum);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double sm = wave_sum(vals[k]);
+    if (lane == 0) psum[(int64_t)blockIdx.x * 64 + 16 * wv + k] = sm;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mask &= (unsigned)__shfl_xor((int)mask, off, 64);
+  if (lane == 0) mq[wv] = (unsigned long long)(mask & 0xFFFFu) << (16 * wv);
+  __syncthreads();
+  if (threadIdx.x == 0) pmask[blockIdx.x] = ((mq[0] | mq[1]) | mq[2]) | mq[3];
 }
 
 // SOCP cones: one workgroup per cone.  lhs_r(a) = lhs_r + a dlhs_r; rhs(a) = rhs + a drhs;
@@ -501,23 +517,48 @@ __global__ __launch_bounds__(256) void k_ls_cone(SocpView v, const double* __res
   }
 }
 
-// final fold of partials (fixed order)
-__global__ __launch_bounds__(64) void k_ls_fold(int64_t nblk, const unsigned long long* __restrict__ pmask,
-                                                const double* __restrict__ psum,
-                                                unsigned long long* __restrict__ mask_out,
-                                                double* __restrict__ sum_out) {
-  const int k = threadIdx.x;
+// final fold of partials (fixed order): 16 groups of 64 threads each sum a contiguous range of
+// partials in order (loads batched), then the group sums are added in group order
+__global__ __launch_bounds__(1024) void k_ls_fold(int64_t nblk, const unsigned long long* __restrict__ pmask,
+                                                  const double* __restrict__ psum,
+                                                  unsigned long long* __restrict__ mask_out,
+                                                  double* __restrict__ sum_out) {
+  __shared__ double red[16][64];
+  __shared__ unsigned long long mred[16];
+  const int k = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t chunk = (nblk + 15) / 16, b0 = g * chunk, b1 = min(nblk, b0 + chunk);
   double s = 0.0;
-  for (int64_t b = 0; b < nblk; ++b) s += psum[b * 64 + k];
-  sum_out[k] = s;
-  if (k == 0) {
-    unsigned long long m = ~0ull;
-    for (int64_t b = 0; b < nblk; ++b) m &= pmask[b];
-    *mask_out = m;
+  int64_t b = b0;
+  for (; b + 8 <= b1; b += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = psum[(b + q) * 64 + k];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; b < b1; ++b) s += psum[b * 64 + k];
+  red[g][k] = s;
+  unsigned long long m = ~0ull;
+  for (int64_t c = b0 + k; c < b1; c += 64) m &= pmask[c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m &= (unsigned long long)__shfl_xor((long long)m, off, 64);
+  if (k == 0) mred[g] = m;
+  __syncthreads();
+  if (g == 0) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][k];
+    sum_out[k] = t;
+    if (k == 0) {
+      unsigned long long mm = ~0ull;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) mm &= mred[q];
+      *mask_out = mm;
+    }
   }
 }
 
-int64_t ls_lin_blocks(int64_t len) { return std::max<int64_t>(1, cdiv(len, 256)); }
+int64_t ls_lin_blocks(int64_t len) { return std::max<int64_t>(1, cdiv(len, LS_EPB)); }
 
 void ls_lin(hipStream_t st, int64_t len, int64_t bar_len, const double* s0, const double* ds, double alpha0,
             double beta, unsigned long long* pmask, double* psum) {
@@ -534,7 +575,7 @@ void ls_cone(hipStream_t st, const SocpView& v, const double* lhs, const double*
 
 void ls_fold(hipStream_t st, int64_t nblk, const unsigned long long* pmask, const double* psum,
              unsigned long long* mask_out, double* sum_out) {
-  hipLaunchKernelGGL(k_ls_fold, dim3(1), dim3(64), 0, st, nblk, pmask, psum, mask_out, sum_out);
+  hipLaunchKernelGGL(k_ls_fold, dim3(1), dim3(1024), 0, st, nblk, pmask, psum, mask_out, sum_out);
 }
 
 // infeasible-start residual candidates (NewtonSolverInfeasibleStart.py:209-269):

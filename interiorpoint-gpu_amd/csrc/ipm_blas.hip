@@ -92,7 +92,15 @@ __global__ __launch_bounds__(256) void k_gemv_t_fin(int64_t cols, int64_t nchunk
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= cols) return;
   double s = 0.0;
-  for (int64_t c = 0; c < nchunk; ++c) s += part[c * cols + j];
+  int64_t c = 0;
+  for (; c + 8 <= nchunk; c += 8) {   // loads batched, sums in chunk order
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = part[(c + q) * cols + j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; c < nchunk; ++c) s += part[c * cols + j];
   y[j] = (beta == 0.0) ? alpha * s : alpha * s + beta * y[j];
 }
 
@@ -1255,16 +1263,31 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
 static constexpr int64_t PANEL_WS = PF_DINV + 36 * 256;
 
+// zero two word ranges in one launch (replaces two hipMemsetAsync calls on the hot path)
+__global__ void k_zero2(unsigned* a, int64_t na, unsigned* b, int64_t nb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < na) a[i] = 0u;
+  else if (i - na < nb) b[i - na] = 0u;
+}
+static void zero2(hipStream_t st, void* a, int64_t na, void* b, int64_t nb) {
+  const int64_t tot = na + nb;
+  if (tot > 0)
+    hipLaunchKernelGGL(k_zero2, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, st, reinterpret_cast<unsigned*>(a), na,
+                       reinterpret_cast<unsigned*>(b), nb);
+}
+
 void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
                        const DeferSyrk* ds) {
   const bool defer = ds && ds->active();
-  hipMemsetAsync(info, 0, sizeof(int), st);
   if (ncols < 0 || ncols > n) ncols = n;
-  if (ncols <= 0) return;
+  if (ncols <= 0) {
+    hipMemsetAsync(info, 0, sizeof(int), st);
+    return;
+  }
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
-  // word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
-  hipMemsetAsync(ctl0, 0, sizeof(unsigned) * (8 + nblocks * cw), st);
+  // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
+  zero2(st, info, 1, ctl0, 8 + nblocks * cw);
   const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     BlockArgs b;

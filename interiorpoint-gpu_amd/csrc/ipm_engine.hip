@@ -31,6 +31,8 @@ using namespace ipm;
 namespace {
 constexpr double STEP_FLOOR = 1e-13;  // NewtonSolver.py:176, 190
 constexpr int NCAND = 64;
+// readback block layout (bytes): info (8 ints), mask (4 words), sums (NCAND), scal (64)
+constexpr int RB_MASK = 32, RB_SUMS = 64, RB_SCAL = RB_SUMS + NCAND * 8;
 constexpr int HOST_WORDS = 4096;
 
 enum Slot {
@@ -205,10 +207,14 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->tmpn = c.take<double>(N);
   pr->tmpp = c.take<double>(p + 1);
   pr->hxs = c.take<double>(N);
-  pr->scal = c.take<double>(64);
-  pr->sums = c.take<double>(NCAND);
-  pr->mask = c.take<unsigned long long>(4);
-  pr->info = c.take<int>(8);
+  // the per-iteration readback block, contiguous (ONE device->host copy): info | mask | sums | scal
+  {
+    char* rb = c.take<char>(RB_SCAL + 64 * 8);
+    pr->info = reinterpret_cast<int*>(rb);
+    pr->mask = reinterpret_cast<unsigned long long*>(rb ? rb + RB_MASK : nullptr);
+    pr->sums = reinterpret_cast<double*>(rb ? rb + RB_SUMS : nullptr);
+    pr->scal = reinterpret_cast<double*>(rb ? rb + RB_SCAL : nullptr);
+  }
   pr->ctl = c.take<unsigned>(8);
   pr->pws = c.take<double>(potrf_ws_doubles(std::max<int64_t>(N + 1, p)));
   pr->coef = c.take<double>(pr->K + 1);
@@ -859,10 +865,7 @@ int readback(ipm_problem* pr, Readback& r, bool want_info) {
   ipm_handle* h = pr->h;
   hipStream_t st = S(pr);
   char* hb = reinterpret_cast<char*>(h->hbuf);
-  hipMemcpyAsync(hb, pr->info, 2 * sizeof(int), hipMemcpyDeviceToHost, st);
-  hipMemcpyAsync(hb + 8, pr->mask, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
-  hipMemcpyAsync(hb + 16, pr->sums, NCAND * sizeof(double), hipMemcpyDeviceToHost, st);
-  hipMemcpyAsync(hb + 16 + NCAND * 8, pr->scal, SC_COUNT * sizeof(double), hipMemcpyDeviceToHost, st);
+  hipMemcpyAsync(hb, pr->info, RB_SCAL + SC_COUNT * sizeof(double), hipMemcpyDeviceToHost, st);
   HIPCHK(h, hipStreamSynchronize(st));
   if (h->timing) {
     float ms = 0.f;
@@ -877,9 +880,9 @@ int readback(ipm_problem* pr, Readback& r, bool want_info) {
   std::memcpy(&r.info, hb, sizeof(int));
   std::memcpy(&r.info2, hb + 4, sizeof(int));
   if (!want_info) r.info = r.info2 = 0;
-  std::memcpy(&r.mask, hb + 8, 8);
-  std::memcpy(r.sums, hb + 16, NCAND * 8);
-  std::memcpy(r.sc, hb + 16 + NCAND * 8, SC_COUNT * 8);
+  std::memcpy(&r.mask, hb + RB_MASK, 8);
+  std::memcpy(r.sums, hb + RB_SUMS, NCAND * 8);
+  std::memcpy(r.sc, hb + RB_SCAL, SC_COUNT * 8);
   return IPM_OK;
 }
 
