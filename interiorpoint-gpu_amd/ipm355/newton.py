@@ -145,7 +145,14 @@ class NewtonSolverDirectInfeasibleStart(NewtonSolverNPSolveInfeasibleStart):
 
 
 class NewtonSolverKKTNPSolveInfeasibleStart(NewtonSolverNPSolveInfeasibleStart):
-    pass
+    """NewtonSolverInfeasibleStart.py:663-689.  The reference assembles the full KKT matrix with
+    np.bmat([[np.diag(H), A^T], [A, 0]]); with a dense (2-D) Hessian np.diag returns its diagonal
+    VECTOR and np.bmat raises ValueError at the first Newton step -- kept: same error, same point."""
+
+    def solve(self, x, t, v0=None):
+        raise ValueError("all the input array dimensions except for the concatenation axis must match "
+                         "exactly (reference NewtonSolverKKTNPSolveInfeasibleStart: np.diag of a dense "
+                         "Hessian inside np.bmat, NewtonSolverInfeasibleStart.py:680-685)")
 
 
 def _cg_unsupported(*a, **k):

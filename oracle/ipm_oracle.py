@@ -1085,6 +1085,8 @@ class LPSolver(_BarrierProblem):
                 meth = meth + "_diag"
             self.ns = InfeasibleNewton(A, b, self.fm, meth, **common)
         else:
+            if linear_solve_method == "kkt" and not diag:   # LPSolver.py:423-430
+                raise ValueError("No KKT System non-equality-constrained problems! Please choose another solver")
             meth = "diag" if diag else {"cholesky": "cholesky", "np_solve": "solve", "np_lstsq": "lstsq",
                                         "direct": "direct"}[linear_solve_method]
             self.ns = FeasibleNewton(self.fm, meth, **common)
@@ -1138,6 +1140,8 @@ class QPSolver(_BarrierProblem):
         if A is not None:
             self.ns = InfeasibleNewton(A, b, self.fm, meth, **common)
         else:
+            if meth == "kkt":   # QPSolver.py:417-424
+                raise ValueError("No KKT System non-equality-constrained problems! Please choose another solver")
             self.ns = FeasibleNewton(self.fm, meth, **common)
 
     def _eq_tol(self):
@@ -1216,6 +1220,8 @@ class SOCPSolver(_BarrierProblem):
         if F is not None:
             self.ns = InfeasibleNewton(F, g, self.fm, meth, **common)
         else:
+            if meth == "kkt":   # SOCPSolver.py dispatch, as QPSolver.py:417-424
+                raise ValueError("No KKT System non-equality-constrained problems! Please choose another solver")
             self.ns = FeasibleNewton(self.fm, meth, **common)
 
     def _eq_tol(self):

@@ -195,3 +195,44 @@ def test_deferred_kkt_slices_match(knobs, monkeypatch):
                                                    list(cpu.inner_iters))
     assert abs(v - v_cpu) <= 1e-8 * max(1.0, abs(v_cpu))
     del v_ref
+
+
+@pytest.mark.parametrize("method", ["np_solve", "np_lstsq", "direct", "kkt"])
+@pytest.mark.parametrize("name", ["qp_ineq_box", "lp_eq_ineq", "qp_eq_phase1"])
+def test_other_linear_solve_methods(name, method):
+    """linear_solve_method other than 'cholesky' (NewtonSolver.py:212-361,
+    NewtonSolverInfeasibleStart.py:279-354, 541-755): device LU against the oracle running the
+    same method (np.linalg.solve / lstsq / inv); x* within 1e-6 relative."""
+    import ipm355
+    from oracle import ipm_oracle as O
+    z = load(name)
+    kw = solver_kwargs(z)
+    kw["x0"] = z["x_init"].copy()
+    kw["linear_solve_method"] = method
+    cls_dev = {"LP": ipm355.LPSolver, "QP": ipm355.QPSolver}[SOLVE_CASES[name]]
+    cls_cpu = {"LP": O.LPSolver, "QP": O.QPSolver}[SOLVE_CASES[name]]
+    if method == "kkt":
+        # the reference rejects it: without equality constraints at construction, with a dense
+        # Hessian at the first Newton step (np.diag of a 2-D Hessian inside np.bmat) -- both ValueError
+        with pytest.raises(ValueError):
+            cls_cpu(**kw).solve()
+        with pytest.raises(ValueError):
+            cls_dev(check_cvxpy=False, suppress_print=True, **kw).solve()
+        return
+    s = cls_dev(check_cvxpy=False, suppress_print=True, **kw)
+    v = s.solve()
+    c = cls_cpu(**kw)
+    vc = c.solve()
+    err = rel(s.xstar, c.xstar)
+    if name == "lp_eq_ineq":
+        # this trajectory passes through Newton steps where backtracking gets stuck on nearly
+        # singular H (t ~ 1e7): there the LU direction is rounding noise of the LU algorithm
+        # itself (LAPACK's blocked recursive dgetrf vs the device's right-looking one), so the
+        # trajectories part; parity is required at the objective (1e-4 relative) and the x*
+        # divergence is reported, not asserted (SURVEY.md §4)
+        print(f"[{name}/{method}] x* rel {err:.1e}, value {v:.10g} vs {vc:.10g}, iters "
+              f"{list(s.inner_iters)} vs {list(c.inner_iters)}")
+        assert abs(v - vc) <= 1e-4 * max(1.0, abs(vc))
+        return
+    assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"])), (err,)
+    assert abs(v - vc) <= max(1e-8, 4 * float(z["sens_value_rel"])) * max(1.0, abs(vc))
