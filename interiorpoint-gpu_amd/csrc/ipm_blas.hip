@@ -907,8 +907,9 @@ struct BlockArgs {
   double* G = nullptr;
   int64_t gldx = 0, ldg = 0, gns = 0, gm = 0;
   int gKS = 0;
-  GemmArgs la32, la, s;          // look-ahead: 32-tiles (rows, cols < 128, lower), 64-tiles (rows >= 128)
-  int nla32 = 0, la32_T = 0;
+  GemmArgs la32, la, la128, s;   // look-ahead: 32-tiles (rows, cols < 128, lower), 64-tiles (rows
+                                 // 128..255, or all rows >= 128 when deferring), 128-tiles (rows >= 256)
+  int nla32 = 0, la32_T = 0, nla64 = 0, nla128 = 0;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
 };
 enum {
@@ -1022,11 +1023,20 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       while ((i + 1) * (i + 2) / 2 <= t) ++i;
       while (i * (i + 1) / 2 > t) --i;
       rb = i >> 1;
-    } else {
+    } else if (t - b.nla32 < b.nla64) {
       const int64_t t64 = t - b.nla32;
       if (b.la.C2) mfma_tile<64, false, VEC, 2, true, true>(b.la, t64, sm.g64);
       else mfma_tile<64, false, VEC, 2, true>(b.la, t64, sm.g64);
       rb = 2 + t64 / b.la_tj;
+    } else {
+      // rows >= 256: 128-tiles (only the later P(a) row chunks wait for them); two 64-row blocks
+      const int64_t t128 = t - b.nla32 - b.nla64;
+      mfma_tile<128, false, VEC, 2, true>(b.la128, t128, sm.g128);
+      rb = 4 + 2 * (t128 / b.la128.tiles_j);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0 && rb + 1 < b.nlab)
+        __hip_atomic_fetch_add(&la_done[rb + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1040,8 +1050,9 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     const int64_t q0 = r0 / 64, q1 = std::min<int64_t>(r1 / 64, b.nlab - 1);
     if (threadIdx.x == 0)
       for (int64_t q = q0; q <= q1; ++q) {
-        // tiles per 64-row block: 32-tile tri rows 2q, 2q+1 (q < 2), else one row of 64-tiles
-        unsigned tgt = (unsigned)b.la_tj;
+        // tiles per 64-row block: 32-tile tri rows 2q, 2q+1 (q < 2), one row of 64-tiles (q < 4
+        // or without 128-tiles), else one row of 128-tiles
+        unsigned tgt = (q < 4 || b.nla128 == 0) ? (unsigned)b.la_tj : (unsigned)b.la128.tiles_j;
         if (q < 2) {
           tgt = 0;
           for (int64_t i = 2 * q; i < 2 * q + 2 && i < b.la32_T; ++i) tgt += (unsigned)(i + 1);
@@ -1323,9 +1334,12 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       c.nblk = c.tiles_i * (c.tiles_i + 1) / 2;
       b.nla32 = (int)c.nblk;
       b.la32_T = (int)c.tiles_i;
-      // rows [128, ni) x all wb columns: 64-tiles, row blocks in order
+      // rows [128, 256) x all wb columns: 64-tiles, row blocks in order (P(b)'s diagonal rows: on
+      // the chain); rows >= 256: 128-tiles (IPM_LA128=0: 64-tiles throughout, as when deferring)
+      static const bool la128_on = [] { const char* e = getenv("IPM_LA128"); return !e || e[0] != '0'; }();
+      const bool use128 = la128_on && !(defer && bk < ds->nblocks && ds->d[bk] > 0);
       GemmArgs& a = b.la;
-      a.ni = std::max<int64_t>(ni - 128, 0);
+      a.ni = std::max<int64_t>((use128 ? std::min<int64_t>(ni, 256) : ni) - 128, 0);
       a.nj = wb;
       a.K = CH_NB;
       a.X = A + cp * lda + cb + 128;
@@ -1339,7 +1353,19 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       a.tiles_i = cdiv(a.ni, 64);
       a.tiles_j = cdiv(a.nj, 64);
       a.nblk = a.tiles_i * a.tiles_j;
-      b.nla = b.nla32 + (int)a.nblk;
+      b.nla64 = (int)a.nblk;
+      if (use128 && ni > 256) {
+        GemmArgs& e = b.la128;
+        e = a;
+        e.ni = ni - 256;
+        e.X = A + cp * lda + cb + 256;
+        e.C = A + cb * lda + cb + 256;
+        e.tiles_i = cdiv(e.ni, 128);
+        e.tiles_j = cdiv(e.nj, 128);
+        e.nblk = e.tiles_i * e.tiles_j;
+        b.nla128 = (int)e.nblk;
+      }
+      b.nla = b.nla32 + b.nla64 + b.nla128;
       b.la_tj = (int)a.tiles_j;
       b.nlab = (int)cdiv(ni, 64);
       if (defer && bk < ds->nblocks && ds->d[bk] > 0 && cb < ds->ns) {
