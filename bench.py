@@ -13,8 +13,9 @@ N > 1: one process per GPU (torchrun), each rank solves its own instance
 (seed = rank) -- independent instances, no data-path collective ("scaling":
 "weak"); rank 0 gathers per-rank times/objectives with one all_gather at the end.
 
-Also reported: the dominant kernel's roofline (the KKT SYRK, fp64 MFMA), the
-Cholesky rate, and the CPU oracle timed on a bounded sample of the same workload.
+Also reported: the dominant kernel's roofline (the Cholesky k_potrf_block, fp64 MFMA),
+the KKT SYRK beside it, the KKT+POTRF kernel-only fp64 fraction, and
+the CPU oracle timed on a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -243,6 +244,9 @@ def main():
                          "traffic": pmc_traffic(PMC_SYRK, n, m),
                          "algorithmic_bytes_per_launch": 8 * (m * n + m + n * (n + 1) / 2 * 2)},
             "potrf": {"achieved_tflops": potrf_tf, "avg_ms": float(allst[0, 3]), "flops": pf},
+            # SURVEY.md §8(d) / BASELINE.md: KKT assembly + Cholesky, kernel time only (HIP events)
+            "kkt_potrf_kernel_frac": ((syrk_flops + pf) / ((float(allst[0, 2]) + float(allst[0, 3])) * 1e-3)
+                                      / 1e12 / FP64_MFMA_PEAK_TFLOPS) if allst[0, 2] + allst[0, 3] > 0 else 0.0,
             "whole_iteration_fp64_frac": (f_iter * total_iters / world / tmax) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "newton_iters": total_iters,
         }

@@ -545,8 +545,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   // Left-looking with one block column of look-ahead: term P (block column P of L, final after
   // step 3 of iteration P) reaches block column P+1 in step 1 of iteration P+1 (4 MFMAs per
   // tile; for the diagonal tile that is all the chain waits for); block column J+1 receives
-  // terms 0..J-1 during the leaf of iteration J (waves 1-2, off the chain).
-  for (int J = 0; J < 8; ++J) {
+  // terms 0..J-1 during the leaf of iteration J (waves 1-2, off the chain).  A partial panel
+  // (the last one) stops after its last 16-column block: beyond nb there is only identity padding.
+  const int nJ = (nb + 15) >> 4;
+  for (int J = 0; J < nJ; ++J) {
     // ---- 1. term J-1 on block column J: wave 0 the diagonal tile, waves 1-3 the tiles below
     if (J > 0) {
       for (int tI = (wv == 0 ? 0 : wv); tI < 8 - J; tI += (wv == 0 ? 8 : 3)) tile_update(J + tI, J, J - 1);
@@ -661,13 +663,16 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     }
     return;
   }
-  if (wv == 3) tri_inverse16(&sD[bidx(7, 7) * 256], &srinv[7 * 16], dinv_out + 7 * 256, lane, pubL != nullptr);
-  if (wv == 2 && pubL) {
-    const int db = bidx(7, 7) * 256;
+  {
+    const int Jl = nJ - 1;   // the last block column (7 for a full panel)
+    if (wv == 3) tri_inverse16(&sD[bidx(Jl, Jl) * 256], &srinv[Jl * 16], dinv_out + Jl * 256, lane, pubL != nullptr);
+    if (wv == 2 && pubL) {
+      const int db = bidx(Jl, Jl) * 256;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
+      for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
+    }
+    if (wv == 1) write_back(Jl, 0, 1);   // (block columns 0 .. Jl-1 went back during the loop)
   }
-  if (wv == 1) write_back(7, 0, 1);   // (block columns 0..6 went back during the loop)
   if (pubL) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -706,9 +711,12 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
       b[J][r] = (rin && c < nb) ? (FUSED ? ld_sc1(&A[(k0 + c) * lda + row]) : A[(k0 + c) * lda + row]) : 0.0;
     }
   dbl4 x[8];
+#pragma unroll
+  for (int J = 0; J < 8; ++J) x[J] = dbl4{0.0, 0.0, 0.0, 0.0};
   unsigned known = 0;
 #pragma unroll
   for (int J = 0; J < 8; ++J) {
+    if (16 * J >= nb) break;   // a partial panel's diagonal role stops at its last block column
     while (known <= (unsigned)J) {
       known = ld_ctl(progress);
       if (known <= (unsigned)J) __builtin_amdgcn_s_sleep(2);
