@@ -919,6 +919,12 @@ struct BlockArgs {
                                  // 128..255, or all rows >= 128 when deferring), 128-tiles (rows >= 256)
   int nla32 = 0, la32_T = 0, nla64 = 0, nla128 = 0;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
+  // ragged trailing rows (IPM_RAG, default on): the last rag_n <= 8 rows of the trailing update,
+  // [rag_r0, rag_r0 + rag_n) relative to its origin, are updated by nrag row workgroups (one
+  // K = 256 dot product per element) instead of a row of 128-tiles (the bordered Newton system
+  // has 1-2 rows past a multiple of 128)
+  int64_t rag_r0 = 0;
+  int rag_n = 0, nrag = 0;
 };
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
@@ -1076,7 +1082,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   // dispatched after the S tiles they do not hold slots the trailing update could use.  Decode first, then ONE call site per role (each role's code
   // is inlined once: register pressure and code size).
   const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_GS, K_NONE } kind = K_NONE;
+  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_GS, K_RAG, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
   if (t == 0) {
@@ -1094,7 +1100,9 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     } else {
       if (b.wbw > 0) t -= 1;
       const int64_t na = b.nra - nchd;
-      if (t < b.ns) {
+      if (t < b.nrag) {
+        kind = K_RAG;
+      } else if ((t -= b.nrag) < b.ns) {
         kind = K_TILE;
       } else if ((t -= b.ns) < na) {
         kind = K_ROW;
@@ -1243,6 +1251,40 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     mfma_tile<64, true, true, 2, false>(g, t - gbase, sm.g64);
     return;
   }
+  if (kind == K_RAG) {
+    ROLE(12);
+    // ragged rows i in [r0, r0 + rn) of the trailing update (origin o, K = the previous block's
+    // 256 columns): C(i, j) -= sum_k L(i, k) L(j, k) for j <= i; workgroup t takes columns
+    // j = 256 t + tid.  Nothing else in this launch touches these elements.
+    const int64_t o = b.cb + b.wa + b.wbw, cp = b.cb - CH_NB;
+    const int64_t m = b.n - o, r0 = b.rag_r0;
+    const int rn = b.rag_n;
+    double* xr = sm.d.sD;   // xr[q * CH_NB + k] = L(o + r0 + q, cp + k)
+    for (int e = tid; e < rn * CH_NB; e += 256) {
+      const int q = e / CH_NB, k = e - q * CH_NB;
+      xr[e] = b.A[(cp + k) * b.lda + o + r0 + q];
+    }
+    __syncthreads();
+    const int64_t j = t * 256 + tid;
+    if (j < m) {
+      double* cj = b.A + (o + j) * b.lda + o + r0;   // C(r0 + q, j) = cj[q]
+      double acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = (q < rn && j <= r0 + q) ? cj[q] : 0.0;
+      const double* xp = b.A + cp * b.lda + o + j;   // L(o + j, cp + k) = xp[k * lda]
+#pragma unroll 16
+      for (int k = 0; k < CH_NB; ++k) {
+        const double xj = xp[k * b.lda];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q < rn) acc[q] = fma(-xj, xr[q * CH_NB + k], acc[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q < rn && j <= r0 + q) cj[q] = acc[q];
+    }
+    return;
+  }
   if (kind == K_TILE) {
     ROLE(4);
     // A trailing tile that lands on the CU of a running critical-path role hands its tile to
@@ -1308,6 +1350,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
   zero2(st, info, 1, ctl0, 8 + nblocks * cw);
   const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
+  // IPM_RAG=0: ragged trailing rows as a row of 128-tiles (read per call: tests compare both)
+  const char* erag = getenv("IPM_RAG");
+  const bool rag_on = !(erag && erag[0] == '0');
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     BlockArgs b;
     b.n = n;
@@ -1389,7 +1434,14 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int64_t m = n - cb - wb;
       if (m > 0) {
         GemmArgs& g = b.s;
-        g.ni = g.nj = m;
+        int64_t ms = m;   // tile rows of the trailing update (ragged rows split off below)
+        if (rag_on && m > 128 && (m & 127) != 0 && (m & 127) <= 8) {
+          ms = m - (m & 127);
+          b.rag_r0 = ms;
+          b.rag_n = (int)(m & 127);
+          b.nrag = (int)cdiv(m, 256);
+        }
+        g.ni = g.nj = ms;
         g.K = CH_NB;
         g.X = g.Y = A + cp * lda + cb + wb;
         g.ldx = g.ldy = lda;
@@ -1402,7 +1454,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         static const int smap = [] { const char* e = getenv("IPM_S_MAP"); return e ? atoi(e) : 0; }();
         b.s_map = smap;
         g.xcd_remap = smap == 0 ? 1 : 0;
-        g.tiles_i = cdiv(m, 128);
+        g.tiles_i = cdiv(ms, 128);
         g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
         b.ns = g.nblk;
       }
@@ -1443,7 +1495,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       }
       b.gs_total = b.gs_cum[b.ngs];
     }
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.ns + b.gs_total;
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
     if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
     else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
   }

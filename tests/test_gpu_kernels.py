@@ -117,3 +117,30 @@ def test_potrs_single_rhs_persistent_solve(n):
     # repeated calls reuse the control words (reset per call)
     x2 = potrs(Hm, n, n, b.copy()).ravel()
     np.testing.assert_array_equal(x, x2)
+
+
+@pytest.mark.parametrize("n,ncols", [(8194, 8193), (1030, 1030), (2690, 2689)])
+def test_potrf_ragged_rows(n, ncols, monkeypatch):
+    """The 1-8 trailing rows past a multiple of 128 (the bordered Newton system) are updated by
+    row workgroups (IPM_RAG, default) instead of a row of 128-tiles: same factor to fp64 rounding
+    as the tile path, and torch's Cholesky / triangular solve to 1e-10."""
+    import torch
+    from gpu_util import potrf as P
+    g = torch.Generator(device="cuda").manual_seed(n)
+    M = torch.rand((n + 5, n), dtype=torch.float64, device="cuda", generator=g) - 0.5
+    A = M.T @ M + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IPM_RAG", mode)
+        H = A.clone()   # symmetric: the column-major buffer is A itself
+        rc, info = P(H, n, n, ncols=ncols)
+        assert rc == 0 and info == 0
+        out[mode] = torch.tril(H.T)[:, :ncols]
+    scale = out["0"].abs().max()
+    assert ((out["1"] - out["0"]).abs().max() / scale).item() < 1e-12
+    L11 = torch.linalg.cholesky(A[:ncols, :ncols])
+    got = out["1"]
+    assert ((got[:ncols] - L11).abs().max() / L11.abs().max()).item() < 1e-10
+    if ncols < n:
+        L21 = torch.linalg.solve_triangular(L11, A[ncols:, :ncols].T, upper=False).T
+        assert ((got[ncols:] - L21).abs().max() / L21.abs().max()).item() < 1e-10
