@@ -1,28 +1,40 @@
 """Benchmark: Newton iterations/sec on the dense QP n=8192, m=2048 (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192] [--m 2048]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192] [--m 2048] [--instances I]
 
-A "step" is one Newton iteration of the real QPSolver.solve() (phase 1 first,
-exactly as the reference runs it: x0 = 0 is infeasible for d = C x_f + 1), on the
-synthetic M3-QP instance of SURVEY.md §8(d) (testSolver.py:499-582 generator and
-kwargs).  W untimed iterations on one solver, then EXACTLY K timed iterations on
-a fresh solver of the same instance (iteration budget), bracketed by barrier +
-synchronize.  Inputs are resident in HBM before the timed region.
+A "step" is one Newton iteration of the real QPSolver.solve() on the synthetic M3-QP instance of
+SURVEY.md §8(d) (testSolver.py:499-582 generator and kwargs; U(-2,2) values on a 2^-10 grid, so
+the rank-0 instance is exactly the one tests/golden/m3_qp_*.npz pins against the reference).
+The K timed steps per instance are split over the two phases the reference runs:
+* ceil(K/2) phase-1 iterations: QPSolver.solve() from the default x0 = 0, which is infeasible for
+  d = C x_f + 1, so phase 1 runs first (bordered n+1 KKT system, PhaseOneSolver.py);
+* floor(K/2) barrier-phase iterations: QPSolver.solve() from the strictly feasible x_f (phase 1
+  skipped), i.e. the centering steps with the tP Hessian term and the P x GEMVs (QPSolver.py:500-638).
+Each segment runs on fresh solvers built (inputs resident in HBM) before its timed region, which is
+bracketed by barrier + synchronize; the reported time is the max over ranks of the two segments'
+sum.  W untimed warmup iterations run first on throw-away solvers (split the same way).
 
-N > 1: one process per GPU (torchrun), each rank solves its own instance
-(seed = rank) -- independent instances, no data-path collective ("scaling":
-"weak"); rank 0 gathers per-rank times/objectives with one all_gather at the end.
+N > 1: one process per GPU.  Without torchrun (WORLD_SIZE unset) `--gpus N` spawns the N ranks
+itself BEFORE touching the GPU (RANK/LOCAL_RANK/WORLD_SIZE set per child).  Independent instances,
+no data-path collective ("scaling": "weak"): rank r solves seed r (headline) or the instances
+r::N of the batch (--instances I: I per GPU, seeds 1000 + index, config 4); rank 0 gathers
+per-rank times with one all_gather at the end (RCCL when every rank has its own GPU, gloo when
+ranks share one -- rehearsals on a 1-GPU box).
 
-Also reported: the dominant kernel's roofline (the Cholesky k_potrf_block, fp64 MFMA),
-the KKT SYRK beside it, the KKT+POTRF kernel-only fp64 fraction, and
-the CPU oracle timed on a bounded sample of the same workload.
+Also reported: the dominant kernel's roofline (the Cholesky k_potrf_block, fp64 MFMA), the KKT SYRK
+beside it, the KKT+POTRF kernel-only fp64 fraction, the committed PMC traffic and
+MFMA counters when they were collected on this exact library build, and the CPU oracle timed on a
+bounded sample of the same workload at 1 and all available BLAS threads.
 """
 from __future__ import annotations
 
 import argparse
 import contextlib
+import hashlib
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -35,19 +47,30 @@ import numpy as np  # noqa: E402
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (256 CU x 2.4 GHz x 128)
 HBM_PEAK_GBS = 8000.0
-# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate passes,
-# FETCH doubled per MI355X_MICROARCH.md) of this same bench: scripts/pmc_summary.py
+LIB = os.path.join(REPO, "interiorpoint-gpu_amd", "ipm355", "libipm355.so")
+# PMC profiles of this bench (scripts/pmc_summary.py): HBM bytes per launch (FETCH_SIZE and
+# WRITE_SIZE in separate passes, FETCH doubled per MI355X_MICROARCH.md) and MFMA busy cycles
 PMC_SYRK = os.path.join(REPO, "profiles", "pmc_kkt_syrk.json")
 PMC_POTRF = os.path.join(REPO, "profiles", "pmc_potrf_block.json")
 
 
-def pmc_traffic(path, n, m):
-    """PMC-measured HBM bytes per launch, only if the committed profile is of this (n, m)."""
+def lib_digest(path=LIB):
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
+def pmc_record(path, n, m):
+    """A committed PMC summary, only if it was collected on this (n, m) AND this exact library
+    build (sha256 of libipm355.so recorded by scripts/pmc_summary.py); stale files are refused."""
     try:
         d = json.load(open(path))
-        return float(d["hbm_bytes_per_launch"]) if (d.get("n"), d.get("m")) == (n, m) else None
     except Exception:
         return None
+    if (d.get("n"), d.get("m")) != (n, m) or d.get("lib_sha256") != lib_digest():
+        return None
+    return d
 
 
 def trailing_bytes(N, nb=256):
@@ -65,63 +88,106 @@ def potrf_flops(N):
     return N ** 3 / 3 + N ** 2 / 2 + N / 6
 
 
-def make_instance(n, m, seed, dev):
-    """M3-QP instance; P = Pp^T Pp + I formed on the device (setup only, not timed)."""
+def launch_ranks(n):
+    """Parent of a self-launched N-rank run: no GPU call happens here (device_count does not
+    initialise the runtime on this image); each child is a fresh process owning LOCAL_RANK."""
     import torch
-    rng = np.random.default_rng(seed)
-    Pp = torch.as_tensor(rng.uniform(-2, 2, size=(int(0.8 * n), n)), device=dev)
-    P = (Pp.T @ Pp).cpu().numpy()
-    del Pp
-    P[np.diag_indices(n)] += 1.0
-    q = rng.uniform(-2, 2, size=n)
-    C = rng.uniform(-2, 2, size=(m, n))
-    xf = rng.uniform(-2, 2, size=n)
-    d = C @ xf + 1
-    return dict(P=P, q=q, C=C, d=d, lower_bound=-3, upper_bound=3)
+
+    from ipm355 import dist as D
+    ndev = torch.cuda.device_count()
+    backend = "nccl" if 0 < n <= ndev else "gloo"
+    return D.launch_local(n, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                          extra_env={"IPM_BENCH_BACKEND": backend})
 
 
-def cpu_baseline(inst, kwargs, seconds=15.0):
-    """Oracle (NumPy/SciPy restatement, oracle/ipm_oracle.py) on a bounded sample of the same
-    workload: phase-1 Newton iterations of this instance, until ~`seconds` of CPU work."""
-    from oracle import ipm_oracle as O
+def make_instance(n, m, seed, dev):
+    """M3-QP instance (grid values); P = Pp^T Pp + I with the Gram product on the device (setup only,
+    exact on the grid, not timed)."""
+    import torch
+    from ipm355 import problems
+
+    def gram(Pp):
+        t = torch.as_tensor(Pp, device=dev)
+        return (t.T @ t).cpu().numpy()
+    inst = problems.qp_ineq_box(n, m, seed=seed, grid=True, with_xf=True, gram=gram)
+    xf = inst.pop("xf")
+    return inst, xf
+
+
+def blas_info():
     try:
         from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
-                      or [1])
+        for i in threadpool_info():
+            if i.get("user_api") == "blas":
+                return {"internal_api": i.get("internal_api"), "version": i.get("version"),
+                        "architecture": i.get("architecture"), "max_threads": i.get("num_threads")}
     except Exception:
-        threads = int(os.environ.get("OPENBLAS_NUM_THREADS", "1"))
+        pass
+    return {}
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        d = dict(line.split(":", 1) for line in out.splitlines() if ":" in line)
+        return {k: d.get(k, "").strip() for k in ("Model name", "Socket(s)", "Core(s) per socket",
+                                                    "Thread(s) per core", "CPU(s)")}
+    except Exception:
+        return {}
+
+
+def cpu_baseline(inst, kwargs, seconds):
+    """Oracle (NumPy/SciPy restatement, oracle/ipm_oracle.py) on a bounded sample of the same
+    workload: phase-1 Newton iterations of this instance (bordered n+1 SYRK + Cholesky + solves),
+    at 1 BLAS thread and at every thread this process may use, ~`seconds` each (>= 1 iteration)."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ipm_oracle as O
     n = len(inst["q"])
     lb = np.array(inst["lower_bound"], dtype=float)
     ub = np.array(inst["upper_bound"], dtype=float)
-    x0 = O.default_x0(n, lb, ub)
-    ph = O.PhaseOne(C=inst["C"], d=inst["d"], lb=lb, ub=ub, x0=x0, max_outer_iters=1,
-                    max_inner_iters=1, epsilon=kwargs["epsilon"], inner_epsilon=1e-5,
-                    alpha=kwargs["alpha"], beta=kwargs["beta"], mu=kwargs["mu"], t0=0.01, n=n, tol=0)
-    iters, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and iters < 200:
-        ph.x, _, k, _, _ = ph.ns.solve(ph.x, 0.01)
-        iters += k
-    el = time.perf_counter() - t0
-    return {"value": iters / el, "unit": "Newton iters/s", "cores": int(threads), "kind": "port",
-            "sample": f"{iters} phase-1 Newton iterations (bordered n+1={n + 1} KKT, m={len(inst['d'])}) of the "
-                      f"same instance, oracle/ipm_oracle.py on NumPy/OpenBLAS, {el:.1f} s"}
+    avail = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
+    nthreads = sorted({1, max(1, min(avail, cap))})
+    runs = []
+    for nt in nthreads:
+        with threadpool_limits(limits=nt, user_api="blas"):
+            ph = O.PhaseOne(C=inst["C"], d=inst["d"], lb=lb, ub=ub, x0=O.default_x0(n, lb, ub), max_outer_iters=1,
+                            max_inner_iters=1, epsilon=kwargs["epsilon"], inner_epsilon=1e-5,
+                            alpha=kwargs["alpha"], beta=kwargs["beta"], mu=kwargs["mu"], t0=0.01, n=n, tol=0)
+            iters, t0 = 0, time.perf_counter()
+            while (time.perf_counter() - t0 < seconds or iters == 0) and iters < 200:
+                ph.x, _, k, _, _ = ph.ns.solve(ph.x, 0.01)
+                iters += k
+            el = time.perf_counter() - t0
+        runs.append({"threads": nt, "iters": iters, "seconds": el, "value": iters / el})
+    best = runs[-1]
+    return {"value": best["value"], "unit": "Newton iters/s", "cores": best["threads"], "kind": "port",
+            "sample": f"{best['iters']} phase-1 Newton iterations (bordered n+1={n + 1} KKT, m={len(inst['d'])}) of "
+                      f"the same instance, oracle/ipm_oracle.py on NumPy/OpenBLAS, {best['seconds']:.1f} s",
+            "by_threads": runs, "host": {"os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+                                         "lscpu": cpu_model(), "blas": blas_info()}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--n", type=int, default=int(os.environ.get("IPM_BENCH_N", 8192)))
     ap.add_argument("--m", type=int, default=int(os.environ.get("IPM_BENCH_M", 2048)))
-    ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("IPM_BENCH_CPU_S", 15)))
+    ap.add_argument("--cpu-seconds", type=float, default=float(os.environ.get("IPM_BENCH_CPU_S", 12)))
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phase", choices=["both", "phase1", "barrier"], default="both",
+                    help="which phase(s) the timed steps run in (default: half each)")
     ap.add_argument("--concurrent", action="store_true",
                     help="solve the instances concurrently: one HIP stream + host thread each")
     ap.add_argument("--instances", type=int, default=1,
                     help="independent instances per GPU (config 4: --n 2048 --m 512 --instances 8); each runs "
                          "`steps` Newton iterations")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     if args.concurrent:
         # each instance = its stream + its Cholesky panel stream; HIP maps streams onto
         # GPU_MAX_HW_QUEUES hardware queues (4 by default) -- streams sharing a queue serialise.
@@ -133,125 +199,177 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # one rank per GPU; on a node with fewer GPUs than ranks (rehearsals) ranks share them
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    backend = os.environ.get("IPM_BENCH_BACKEND") or ("nccl" if world <= ndev else "gloo")
+    if backend == "nccl" and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} has no GPU of its own ({ndev} visible) under RCCL")
+    dev_index = local % max(ndev, 1)       # gloo rehearsals: ranks share the visible GPU(s)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    sdev = dev if backend == "nccl" else torch.device("cpu")
 
     import ipm355
     from ipm355 import _lib as L
+    from ipm355 import dist as D
     from ipm355 import problems
 
     kwargs = dict(problems.QP_KWARGS)
-    # one instance: seed = rank (headline); several: seeds 1000 + rank * instances + i
-    seeds = [rank] if args.instances == 1 else [1000 + rank * args.instances + i for i in range(args.instances)]
+    if args.instances == 1:
+        seeds = [rank]                         # headline: one n=8192 instance per GPU, seed = rank
+    else:                                      # config 4: instances r::world of world*I, seeds 1000 + index
+        seeds = [1000 + i for i in D.shard(args.instances * world, rank, world)]
     insts = [make_instance(args.n, args.m, seed=sd, dev=dev) for sd in seeds]
 
-    def new_solver(inst):
-        return ipm355.QPSolver(check_cvxpy=False, suppress_print=True, device=local, **inst, **kwargs)
+    def new_solver(k, feasible):
+        inst, xf = insts[k]
+        kw = dict(inst, **kwargs)
+        if feasible:
+            kw["x0"] = xf.copy()               # strictly feasible -> phase 1 skipped (Q11)
+        return ipm355.QPSolver(check_cvxpy=False, suppress_print=True, device=dev_index, **kw)
 
-    # one stream per instance when concurrent (solvers bind their handle to the current stream)
     streams = [torch.cuda.Stream(device=dev) for _ in insts] if args.concurrent else [None] * len(insts)
 
     def on(stream):
         return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
-    # warmup: W iterations on a throw-away solver per stream (kernels, allocator, caches)
-    if args.warmup > 0:
-        for inst, stm in zip(insts, streams if args.concurrent else streams[:1]):
-            with on(stm):
-                new_solver(inst).solve(iteration_budget=args.warmup)
-    solvers = []
-    for inst, stm in zip(insts, streams):                 # inputs resident in HBM before timing
-        with on(stm):
-            solvers.append(new_solver(inst))
+    k1 = {"both": (args.steps + 1) // 2, "phase1": args.steps, "barrier": 0}[args.phase]
+    segs = [("phase1", k1), ("barrier", args.steps - k1)]
+    w1 = (args.warmup + 1) // 2
+    for feasible, budget in ((False, w1), (True, args.warmup - w1)):   # warmup, untimed
+        if budget > 0:
+            for k in range(len(insts) if args.concurrent else 1):
+                with on(streams[k]):
+                    new_solver(k, feasible).solve(iteration_budget=budget)
     with on(streams[0]):
-        h = L.Handle.get(local)
-    h.lib.ipm_set_timing(h.ptr, 1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    if args.concurrent:
-        from concurrent.futures import ThreadPoolExecutor
-
-        def run(k):
-            with on(streams[k]):
-                solvers[k].solve(iteration_budget=args.steps)
-        with ThreadPoolExecutor(max_workers=len(solvers)) as ex:
-            list(ex.map(run, range(len(solvers))))
-    else:
-        for solver in solvers:
-            solver.solve(iteration_budget=args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+        h = L.Handle.get(dev_index)
     import ctypes
-    a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-    h.lib.ipm_last_timings(h.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
-    kkt_ms, potrf_ms, cnt = a.value, b.value, c.value
-    p1 = sum(sum(s.phase1_solver.inner_iters) for s in solvers)
-    done = p1 + sum(sum(s.inner_iters) for s in solvers)
-    inst = insts[0]
+    res = {}
+    for name, budget in segs:
+        if budget <= 0:
+            res[name] = dict(iters=0, seconds=0.0, kkt_ms=0.0, potrf_ms=0.0, kkt_flops=0.0, N=0)
+            continue
+        solvers = []
+        for k, stm in enumerate(streams):           # inputs resident in HBM before timing
+            with on(stm):
+                solvers.append(new_solver(k, name == "barrier"))
+        fm0 = solvers[0].phase1_solver.phase1_fm if name == "phase1" else solvers[0].fm
+        kkt_flops = fm0.prob.kkt_flops()[0]
+        h.lib.ipm_set_timing(h.ptr, 1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        if args.concurrent:
+            from concurrent.futures import ThreadPoolExecutor
 
-    stats = torch.tensor([el, float(done), kkt_ms, potrf_ms, float(p1)], dtype=torch.float64, device=dev)
+            def run(k):
+                with on(streams[k]):
+                    solvers[k].solve(iteration_budget=budget)
+            with ThreadPoolExecutor(max_workers=len(solvers)) as ex:
+                list(ex.map(run, range(len(solvers))))
+        else:
+            for s in solvers:
+                s.solve(iteration_budget=budget)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        h.lib.ipm_last_timings(h.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        iters = 0
+        for s in solvers:
+            p1 = s.phase1_solver
+            iters += sum(s.inner_iters) + (sum(p1.inner_iters) if p1 is not None and name == "phase1" else 0)
+        res[name] = dict(iters=float(iters), seconds=el, kkt_ms=a.value, potrf_ms=b.value, kkt_flops=kkt_flops,
+                         N=args.n + (1 if name == "phase1" else 0))
+        del solvers
+
+    keys = ("iters", "seconds", "kkt_ms", "potrf_ms")
+    row = [res[nm][k] for nm, _ in segs for k in keys]
+    stats = torch.tensor(row, dtype=torch.float64, device=sdev)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
-        dist.all_gather(allst, stats)          # the only collective: end-of-run gather over xGMI
+        dist.all_gather(allst, stats)          # the only collective: end-of-run gather
         allst = torch.stack(allst).cpu().numpy()
     else:
         allst = stats.cpu().numpy()[None]
     if rank == 0:
-        tmax = float(allst[:, 0].max())
-        total_iters = float(allst[:, 1].sum())
         n, m = args.n, args.m
-        syrk_flops = m * n * (n + 1) + n * n      # Cholesky-KKT assembly: SYRK + tP epilogue
-        # phase-1 iterations factor the (n+1)-variable system, the others n (rank 0's mix)
-        f1 = float(allst[0, 4]) / max(float(allst[0, 1]), 1.0)
-        pf = f1 * potrf_flops(n + 1) + (1 - f1) * potrf_flops(n)
-        launches = f1 * ((n + 1 + 255) // 256) + (1 - f1) * ((n + 255) // 256)   # one per 256 columns
-        kkt_tf = syrk_flops / (float(allst[0, 2]) * 1e-3) / 1e12 if allst[0, 2] > 0 else 0.0
-        potrf_tf = pf / (float(allst[0, 3]) * 1e-3) / 1e12 if allst[0, 3] > 0 else 0.0
-        f_iter = m * n * (n + 1) + pf + 2 * n * n
+        per = {}
+        for j, (nm, _) in enumerate(segs):
+            blk = allst[:, 4 * j:4 * j + 4]
+            per[nm] = dict(iters=float(blk[:, 0].sum()), tmax=float(blk[:, 1].max()), rank_seconds=blk[:, 1],
+                           kkt_ms=float(blk[0, 2]), potrf_ms=float(blk[0, 3]))
+        rank_total = sum(per[nm]["rank_seconds"] for nm, _ in segs)
+        tmax = float(np.max(rank_total))
+        total_iters = sum(per[nm]["iters"] for nm, _ in segs)
+        # rank 0's kernel timings, weighted by its per-segment iteration counts
+        it0 = {nm: float(allst[0, 4 * j]) for j, (nm, _) in enumerate(segs)}
+        tot0 = max(sum(it0.values()), 1.0)
+        pf_tot = sum(it0[nm] * potrf_flops(res[nm]["N"]) for nm, _ in segs if it0[nm])
+        pt_tot = sum(it0[nm] * per[nm]["potrf_ms"] for nm, _ in segs)
+        launches = sum(it0[nm] * math.ceil(res[nm]["N"] / 256) for nm, _ in segs)
+        kf_tot = sum(it0[nm] * res[nm]["kkt_flops"] for nm, _ in segs)
+        kt_tot = sum(it0[nm] * per[nm]["kkt_ms"] for nm, _ in segs)
+        potrf_tf = pf_tot / (pt_tot * 1e-3) / 1e12 if pt_tot > 0 else 0.0
+        kkt_tf = kf_tot / (kt_tot * 1e-3) / 1e12 if kt_tot > 0 else 0.0
+        f_iter = sum(it0[nm] * (res[nm]["kkt_flops"] + potrf_flops(res[nm]["N"]) + 2 * res[nm]["N"] ** 2)
+                     for nm, _ in segs) / tot0
+        pmc_p, pmc_s = pmc_record(PMC_POTRF, n, m), pmc_record(PMC_SYRK, n, m)
+        Nmain = n + 1 if it0.get("phase1", 0) >= it0.get("barrier", 0) else n
         value = total_iters / tmax
         rec = {
             "metric": "Newton iters/sec, dense QP n=8192, 1/2/4/8 GPUs; achieved % fp64 roofline",
             "value": value, "unit": "Newton iters/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": tmax / max(total_iters / world, 1) * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded M3-QP generator, testSolver.py:499-582 shapes)",
-            "config": {"workload": f"QPSolver.solve() dense QP n={n}, m={m} ineq, box +-3, phase 1 incl., "
-                                   f"test_QP kwargs; {args.instances} independent instance(s) per GPU"
-                                   + (" solved concurrently (one stream + host thread each)" if args.concurrent else ""),
+            "data": "synthetic (seeded M3-QP generator, testSolver.py:499-582 shapes; U(-2,2) on a 2^-10 grid)",
+            "config": {"workload": f"QPSolver.solve() dense QP n={n}, m={m} ineq, box +-3, test_QP kwargs; per "
+                                   f"instance {k1} phase-1 iterations (from x0=0) + {args.steps - k1} barrier-phase "
+                                   f"iterations (from the feasible x_f); {args.instances} independent instance(s) "
+                                   f"per GPU" + (" solved concurrently (one stream + host thread each)"
+                                                 if args.concurrent else ""),
                        "n": n, "m": m, "instances_per_gpu": args.instances,
-                       "parallelism": f"instances{world * args.instances}"},
+                       "parallelism": f"instances{world * args.instances}", "backend": backend if world > 1 else None},
+            "phases": {nm: {"iters": per[nm]["iters"], "seconds_max_rank": per[nm]["tmax"],
+                            "iters_per_s": per[nm]["iters"] / per[nm]["tmax"] if per[nm]["tmax"] > 0 else None,
+                            "kkt_ms": per[nm]["kkt_ms"], "potrf_ms": per[nm]["potrf_ms"],
+                            "system_size": res[nm]["N"]} for nm, _ in segs},
             # dominant kernel: the Cholesky, one k_potrf_block launch per 256 columns; achieved =
             # factorization flops / HIP-event time of all its launches (= per-launch flops / avg launch)
             "roofline": {"bound": "mfma", "achieved": potrf_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": potrf_tf / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(PMC_POTRF, n, m),
+                         "frac": potrf_tf / FP64_MFMA_PEAK_TFLOPS,
+                         "traffic": pmc_p["hbm_bytes_per_launch"] if pmc_p else None,
                          "kernel": "k_potrf_block (blocked Cholesky of the Newton matrix, bordered RHS row)",
-                         "flops_per_launch": pf / launches, "avg_launch_ms": float(allst[0, 3]) / launches,
-                         "launches_per_factorization": launches,
+                         "flops_per_launch": pf_tot / max(launches, 1),
+                         "avg_launch_ms": pt_tot / max(launches, 1),
+                         "launches_per_factorization": launches / tot0,
                          # right-looking blocked Cholesky: each launch reads and writes the lower
                          # trailing matrix once (16 B per element), averaged over the launches
-                         "algorithmic_bytes_per_launch": trailing_bytes(n + 1 if f1 >= 0.5 else n) / launches},
-            "kkt_syrk": {"kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = tP + C^T diag(w) C + diag)",
+                         "algorithmic_bytes_per_launch": trailing_bytes(Nmain) / math.ceil(Nmain / 256),
+                         "mfma_counters": (pmc_p or {}).get("mfma")},
+            "kkt_syrk": {"kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = [tP +] C^T diag(w) C + diag)",
                          "achieved_tflops": kkt_tf, "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS,
-                         "flops_per_launch": syrk_flops, "avg_launch_ms": float(allst[0, 2]),
-                         "traffic": pmc_traffic(PMC_SYRK, n, m),
-                         "algorithmic_bytes_per_launch": 8 * (m * n + m + n * (n + 1) / 2 * 2)},
-            "potrf": {"achieved_tflops": potrf_tf, "avg_ms": float(allst[0, 3]), "flops": pf},
+                         "flops_per_launch": kf_tot / tot0, "avg_launch_ms": kt_tot / tot0,
+                         "traffic": pmc_s["hbm_bytes_per_launch"] if pmc_s else None,
+                         "algorithmic_bytes_per_launch": 8 * (m * n + m + n * (n + 1) / 2 * 2),
+                         "mfma_counters": (pmc_s or {}).get("mfma")},
+            "potrf": {"achieved_tflops": potrf_tf, "avg_ms": pt_tot / tot0, "flops": pf_tot / tot0},
             # SURVEY.md §8(d) / BASELINE.md: KKT assembly + Cholesky, kernel time only (HIP events)
-            "kkt_potrf_kernel_frac": ((syrk_flops + pf) / ((float(allst[0, 2]) + float(allst[0, 3])) * 1e-3)
-                                      / 1e12 / FP64_MFMA_PEAK_TFLOPS) if allst[0, 2] + allst[0, 3] > 0 else 0.0,
+            "kkt_potrf_kernel_frac": ((kf_tot + pf_tot) / ((kt_tot + pt_tot) * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS)
+                                     if kt_tot + pt_tot > 0 else 0.0,
             "whole_iteration_fp64_frac": (f_iter * total_iters / world / tmax) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "newton_iters": total_iters,
+            "lib_sha256": lib_digest(),
         }
         if not args.no_cpu and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(inst, kwargs, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(insts[0][0], kwargs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

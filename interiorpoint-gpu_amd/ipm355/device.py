@@ -84,6 +84,7 @@ class DeviceProblem:
         self.handle = L.Handle.get(device)
         dev = self.handle.torch_device
         self.dev = dev
+        self.hstream = torch.cuda.ExternalStream(self.handle.stream, device=dev)
         self.kind, self.n, self.phase1 = kind, n, phase1
         self.N = n + (1 if phase1 else 0)
         # keep references so the device memory outlives the problem
@@ -143,6 +144,20 @@ class DeviceProblem:
     def check(self, rc):
         self.handle.check(rc, self.handle.ptr)
 
+    def call(self, fn, *args):
+        """Run one native entry point ordered against torch's CURRENT stream: the handle's stream
+        waits for work queued on the caller's stream (e.g. the facade's clone of x), and the caller's
+        stream waits for the native launches before it touches their outputs."""
+        import torch
+        cur = torch.cuda.current_stream(self.dev)
+        other = cur.cuda_stream != self.handle.stream
+        if other:
+            self.hstream.wait_stream(cur)
+        rc = fn(*args)
+        if other:
+            cur.wait_stream(self.hstream)
+        self.check(rc)
+
     # ---- level 2
     def newton_solve(self, x, t, v, *, max_iters, eps, alpha, beta, update_slacks_every=0,
                      phase1_flag=False, phase1_tol=0.0, use_psd_condition=False):
@@ -154,8 +169,8 @@ class DeviceProblem:
         o.trace = ct.cast(buf, ct.POINTER(ct.c_double))
         o.trace_cap = cap
         r = L.NewtonResult()
-        self.check(self.handle.lib.ipm_newton_solve(self.ptr, L.dptr(x), float(t), L.dptr(v), ct.byref(o),
-                                                    ct.byref(r)))
+        self.call(self.handle.lib.ipm_newton_solve, self.ptr, L.dptr(x), float(t), L.dptr(v), ct.byref(o),
+                                                    ct.byref(r))
         k = min(int(r.iters), cap)
         self.last_trace = [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
         return r
@@ -163,7 +178,7 @@ class DeviceProblem:
     def kkt_flops(self):
         """(up-front SYRK flops, flops of the slices deferred into the Cholesky) per Newton step"""
         a, b = ct.c_double(), ct.c_double()
-        self.check(self.handle.lib.ipm_kkt_flops(self.ptr, ct.byref(a), ct.byref(b)))
+        self.call(self.handle.lib.ipm_kkt_flops, self.ptr, ct.byref(a), ct.byref(b))
         return a.value, b.value
 
     @property
@@ -176,37 +191,37 @@ class DeviceProblem:
 
     # ---- level 1 (oracle protocol)
     def fm_update_x(self, x, update_slacks=True):
-        self.check(self.handle.lib.ipm_fm_update_x(self.ptr, L.dptr(x), 1 if update_slacks else 0))
+        self.call(self.handle.lib.ipm_fm_update_x, self.ptr, L.dptr(x), 1 if update_slacks else 0)
 
     def fm_slacks(self):
         import torch
         out = torch.empty(max(self.num_slacks, 0), dtype=torch.float64, device=self.dev)
         if self.num_slacks:
-            self.check(self.handle.lib.ipm_fm_slacks(self.ptr, L.dptr(out)))
+            self.call(self.handle.lib.ipm_fm_slacks, self.ptr, L.dptr(out))
         return out
 
     def fm_objective(self):
         v = ct.c_double()
-        self.check(self.handle.lib.ipm_fm_objective(self.ptr, ct.byref(v)))
+        self.call(self.handle.lib.ipm_fm_objective, self.ptr, ct.byref(v))
         return v.value
 
     def fm_newton_objective(self, t):
         v = ct.c_double()
-        self.check(self.handle.lib.ipm_fm_newton_objective(self.ptr, float(t), ct.byref(v)))
+        self.call(self.handle.lib.ipm_fm_newton_objective, self.ptr, float(t), ct.byref(v))
         return v.value
 
     def fm_gradient(self, t):
         import torch
         g = torch.empty(self.N, dtype=torch.float64, device=self.dev)
-        self.check(self.handle.lib.ipm_fm_gradient(self.ptr, float(t), L.dptr(g)))
+        self.call(self.handle.lib.ipm_fm_gradient, self.ptr, float(t), L.dptr(g))
         return g
 
     def fm_hessian(self, t, diag=False):
         import torch
         if diag:
             H = torch.empty(self.n, dtype=torch.float64, device=self.dev)
-            self.check(self.handle.lib.ipm_fm_hessian(self.ptr, float(t), L.dptr(H), self.n))
+            self.call(self.handle.lib.ipm_fm_hessian, self.ptr, float(t), L.dptr(H), self.n)
             return H
         H = torch.empty((self.N, self.N), dtype=torch.float64, device=self.dev)
-        self.check(self.handle.lib.ipm_fm_hessian(self.ptr, float(t), L.dptr(H), self.N))
+        self.call(self.handle.lib.ipm_fm_hessian, self.ptr, float(t), L.dptr(H), self.N)
         return H

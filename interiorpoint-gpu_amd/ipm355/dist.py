@@ -12,6 +12,8 @@ instance's (objective, Newton iterations, seconds).
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
 import time
 
 import numpy as np
@@ -33,20 +35,43 @@ def _world():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def gather_results(local: dict, n_instances: int, device=None) -> np.ndarray:
+def _backend():
+    import torch.distributed as dist
+    return dist.get_backend() if dist.is_available() and dist.is_initialized() else None
+
+
+def local_device(device=None) -> int:
+    """The GPU this rank owns: the explicit ``device`` or LOCAL_RANK (one process per GPU)."""
+    return int(device) if device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _table_device(device):
+    """RCCL (backend "nccl") gathers device tensors; gloo and the single-process case host ones."""
+    import torch
+    return torch.device("cuda", local_device(device)) if _backend() == "nccl" else torch.device("cpu")
+
+
+def gather_results(local: dict, n_instances: int, device=None, xs: dict | None = None, n: int = 0):
     """all_gather every rank's {index: (value, iters, seconds)} -> (n_instances, 3) array.
 
     Every rank contributes a fixed-size (ceil(n/world), FIELDS) table padded with index -1.
-    This is the only collective of the sharded path.
+    With ``xs`` ({index: x* (n,)}) the x* rows travel in the same collective (appended columns),
+    and the return value is (table, X) with X (n_instances, n).  This is the only collective of
+    the sharded path; under RCCL the table lives on this rank's GPU.
     """
     import torch
     import torch.distributed as dist
     rank, world = _world()
     slots = -(-n_instances // world)
-    tab = torch.full((slots, FIELDS), -1.0, dtype=torch.float64, device=device)
+    width = FIELDS + (n if xs is not None else 0)
+    tab = torch.full((slots, width), -1.0, dtype=torch.float64)
     for k, (idx, vals) in enumerate(sorted(local.items())):
         tab[k, 0] = float(idx)
-        tab[k, 1:] = torch.tensor([float(v) for v in vals], dtype=torch.float64)
+        tab[k, 1:FIELDS] = torch.tensor([float(v) if v is not None else float("nan") for v in vals],
+                                        dtype=torch.float64)
+        if xs is not None:
+            tab[k, FIELDS:] = torch.as_tensor(np.asarray(xs[idx], dtype=np.float64))
+    tab = tab.to(_table_device(device))
     if world > 1 and dist.is_initialized():
         parts = [torch.empty_like(tab) for _ in range(world)]
         dist.all_gather(parts, tab)
@@ -54,30 +79,96 @@ def gather_results(local: dict, n_instances: int, device=None) -> np.ndarray:
     else:
         allt = tab.cpu().numpy()
     out = np.full((n_instances, FIELDS - 1), np.nan)
+    X = np.full((n_instances, n), np.nan) if xs is not None else None
     for row in allt:
         if row[0] >= 0:
-            out[int(row[0])] = row[1:]
-    return out
+            out[int(row[0])] = row[1:FIELDS]
+            if X is not None:
+                X[int(row[0])] = row[FIELDS:]
+    return (out, X) if xs is not None else out
 
 
 def solve_sharded(make_instance, n_instances: int, solver_cls=None, kwargs=None, device=None,
-                  solve_fn=None) -> np.ndarray:
-    """Solve this rank's shard, then gather every instance's (value, iters, seconds).
+                  solve_fn=None, gather_x: bool = False):
+    """Solve this rank's shard on this rank's GPU, then gather every instance's (value, iters, seconds).
 
     make_instance(i) -> dict of constructor arguments for instance i (seeded by i);
     solver_cls: ipm355.LPSolver / QPSolver / SOCPSolver; kwargs: shared solver kwargs.
-    solve_fn(i) -> (value, iters) overrides the solver (host-logic tests run it without a GPU).
+    device: this rank's GPU (default LOCAL_RANK); every solver is built on it.
+    solve_fn(i) -> (value, iters[, x*]) overrides the solver (host-logic tests run it without a GPU).
+    gather_x: also gather every instance's x* -> returns (table, X).
     """
     rank, world = _world()
-    local = {}
+    dev = local_device(device)
+    local, xs = {}, {}
     for i in shard(n_instances, rank, world):
         t0 = time.perf_counter()
         if solve_fn is not None:
-            value, iters = solve_fn(i)
+            r = solve_fn(i)
+            value, iters = r[0], r[1]
+            x = r[2] if len(r) > 2 else None
         else:
-            s = solver_cls(check_cvxpy=False, suppress_print=True, **make_instance(i), **(kwargs or {}))
+            s = solver_cls(check_cvxpy=False, suppress_print=True, device=dev, **make_instance(i),
+                           **(kwargs or {}))
+            if s.dev.index != dev:
+                raise RuntimeError(f"solver placed on {s.dev}, rank owns cuda:{dev}")
             value = s.solve()
             p1 = getattr(s, "phase1_solver", None)
             iters = int(sum(s.inner_iters)) + (int(sum(p1.inner_iters)) if p1 is not None else 0)
+            x = s.xstar
         local[i] = (value, iters, time.perf_counter() - t0)
+        if gather_x:
+            xs[i] = x
+    if gather_x:
+        nx = len(next(iter(xs.values()))) if xs else 0
+        if world > 1 and dist_initialized():
+            import torch
+            import torch.distributed as dist
+            t = torch.tensor([nx], dtype=torch.int64, device=_table_device(device))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            nx = int(t.item())
+        return gather_results(local, n_instances, device=device, xs=xs, n=nx)
     return gather_results(local, n_instances, device=device)
+
+
+def dist_initialized() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_local(nprocs: int, argv: list, extra_env: dict | None = None, poll_s: float = 0.2) -> int:
+    """Start `argv` as `nprocs` fresh rank processes on this node (torchrun's env contract: RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.
+
+    Call it before anything initialises the GPU in this process: children are started, never
+    exec'd.  If one rank fails the others are terminated (they would wait in a barrier forever).
+    Returns 0 or the first failing rank's exit status (128 + signal for a killed rank)."""
+    port = _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                   LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0:
+                rc = rc or (c if c > 0 else 128 - c)
+                for q in procs:
+                    q.terminate()
+        if procs:
+            time.sleep(poll_s)
+    return rc

@@ -29,27 +29,64 @@ def lp_eq_box(n=200, p=50, seed=0):
     return dict(c=c, A=A, b=b, lower_bound=0, upper_bound=3)
 
 
-def lp_ineq_box(n=200, m=50, seed=0):
+GRID = 2.0 ** -10
+
+
+def _u(rng, size, grid):
+    """U(-2, 2); with ``grid`` the values are rounded to multiples of 2^-10.  Every product of two
+    such values is a multiple of 2^-20 and every dot product used by the generators stays below
+    2^15, so it needs at most 35 significand bits: P = Pp'Pp and d = C x_f + 1 are then EXACT in
+    fp64 whatever BLAS, thread count or summation order computes them.  The large parity fixtures
+    (tests/golden/make_golden_large.py) use this so that the GPU box regenerates bit-identical
+    inputs without shipping them."""
+    a = rng.uniform(-2, 2, size=size)
+    return np.round(a / GRID) * GRID if grid else a
+
+
+def lp_ineq_box(n=200, m=50, seed=0, grid=False, with_xf=False):
     """M1b / M3-LP: min c'x s.t. Cx <= d, -3 <= x <= 3 with d = C x_f + 1 (strictly feasible)."""
     rng = np.random.default_rng(seed)
-    C = rng.uniform(-2, 2, size=(m, n))
-    xf = rng.uniform(-2, 2, size=n)
+    C = _u(rng, (m, n), grid)
+    xf = _u(rng, n, grid)
     d = C @ xf + 1
-    c = rng.uniform(-2, 2, size=n)
-    return dict(c=c, C=C, d=d, lower_bound=-3, upper_bound=3)
+    c = _u(rng, n, grid)
+    out = dict(c=c, C=C, d=d, lower_bound=-3, upper_bound=3)
+    if with_xf:
+        out["xf"] = xf
+    return out
 
 
-def qp_ineq_box(n=2048, m=512, seed=0):
-    """M2 / M3-QP / M4: P = Pp'Pp + I (Pp: floor(0.8 n) x n), q, Cx <= d = C x_f + 1, -3 <= x <= 3."""
+def qp_ineq_box(n=2048, m=512, seed=0, grid=False, with_xf=False, gram=None):
+    """M2 / M3-QP / M4: P = Pp'Pp + I (Pp: floor(0.8 n) x n), q, Cx <= d = C x_f + 1, -3 <= x <= 3.
+
+    ``gram(Pp) -> Pp'Pp`` may be supplied (e.g. a device GEMM for n=8192); with ``grid`` any exact
+    product gives the same P bit for bit."""
     rng = np.random.default_rng(seed)
-    Pp = rng.uniform(-2, 2, size=(int(0.8 * n), n))
-    P = Pp.T @ Pp + np.eye(n)
+    Pp = _u(rng, (int(0.8 * n), n), grid)
+    P = gram(Pp) if gram is not None else Pp.T @ Pp
     del Pp
-    q = rng.uniform(-2, 2, size=n)
-    C = rng.uniform(-2, 2, size=(m, n))
-    xf = rng.uniform(-2, 2, size=n)
+    P[np.diag_indices(n)] += 1.0
+    q = _u(rng, n, grid)
+    C = _u(rng, (m, n), grid)
+    xf = _u(rng, n, grid)
     d = C @ xf + 1
-    return dict(P=P, q=q, C=C, d=d, lower_bound=-3, upper_bound=3)
+    out = dict(P=P, q=q, C=C, d=d, lower_bound=-3, upper_bound=3)
+    if with_xf:
+        out["xf"] = xf
+    return out
+
+
+def input_digest(inst):
+    """sha256 over the array inputs of an instance (sorted keys): proves regenerated inputs are the
+    ones a fixture was computed on."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(inst):
+        v = inst[k]
+        if isinstance(v, np.ndarray):
+            h.update(k.encode())
+            h.update(np.ascontiguousarray(v, dtype=np.float64).tobytes())
+    return h.hexdigest()
 
 
 def socp_cones(n=4096, K=256, mi=16, seed=0, eq=0):

@@ -176,6 +176,7 @@ class _BarrierSolver:
                     break
                 self.ns.max_iters = min(self.max_inner_iters, self._budget[0])
             x, v, numiters_t, _, success_flag = self.ns.solve(x, t, v0=v)
+            self.x_last = x              # extension: the current iterate (truncated parity runs)
             if self._budget is not None:
                 self._budget[0] -= numiters_t
                 self.ns.max_iters = self.max_inner_iters

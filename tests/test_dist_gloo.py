@@ -54,3 +54,53 @@ def test_all_gather_results_gloo(tmp_path, world, n):
 def test_single_process_gather_without_init():
     res = D.gather_results({0: (1.0, 2, 0.1), 2: (3.0, 4, 0.2)}, 3)
     assert res[0, 0] == 1.0 and res[2, 1] == 4 and np.isnan(res[1, 0])
+
+
+def test_launch_local_end_to_end(tmp_path):
+    """The self-launcher bench.py --gpus N uses (ipm355.dist.launch_local): N fresh rank processes
+    with torchrun's env contract, solve_sharded over gloo, x* gathered -> every rank has every row."""
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_worker.py")
+    rc = D.launch_local(2, [sys.executable, worker, "9", str(tmp_path)])
+    assert rc == 0
+    for r in range(2):
+        tab = np.load(tmp_path / f"tab{r}.npy")
+        X = np.load(tmp_path / f"x{r}.npy")
+        np.testing.assert_array_equal(tab[:, 0], 100.0 + np.arange(9))
+        np.testing.assert_array_equal(tab[:, 1], 7 + np.arange(9) % 3)
+        np.testing.assert_array_equal(X, np.arange(9)[:, None] * np.arange(5)[None, :])
+        assert (tmp_path / f"env{r}.txt").read_text() == f"{r} {r} 2"
+
+
+def test_launch_local_failing_rank_terminates_the_others(tmp_path):
+    import sys
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(60)\n")
+    rc = D.launch_local(2, [sys.executable, "-c", code])
+    assert rc == 3
+
+
+class _FakeSolver:
+    """Records where solve_sharded places each instance (every rank used GPU 0)."""
+    seen = []
+
+    def __init__(self, device=None, **kw):
+        import types
+        self.dev = types.SimpleNamespace(index=device)
+        _FakeSolver.seen.append(device)
+        self.inner_iters, self.phase1_solver, self.xstar = [3], None, np.zeros(2)
+
+    def solve(self):
+        return 1.5
+
+
+def test_solve_sharded_places_solvers_on_the_rank_device(monkeypatch):
+    _FakeSolver.seen = []
+    monkeypatch.setenv("LOCAL_RANK", "3")
+    res = D.solve_sharded(lambda i: {}, 2, _FakeSolver)
+    assert _FakeSolver.seen == [3, 3]
+    np.testing.assert_array_equal(res[:, 0], [1.5, 1.5])
+    _FakeSolver.seen = []
+    D.solve_sharded(lambda i: {}, 1, _FakeSolver, device=5)
+    assert _FakeSolver.seen == [5]

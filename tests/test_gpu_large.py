@@ -1,0 +1,175 @@
+"""-m gpu: parity at the BASELINE.json sizes.
+
+The fixtures come from the REFERENCE itself (tests/golden/make_golden_large.py, run in the build
+container): instances are regenerated here from their seed with ``grid=True`` (U(-2,2) on a 2^-10
+grid, so P = Pp'Pp and d = C x_f + 1 are exact in fp64 whatever computes them) and checked against
+the sha256 the fixture stores, so the GPU sees exactly the reference's inputs.
+
+Bars (north star: x* within 1e-6 relative of the reference NumPy solve):
+* full solves (M2, the M4 shard): x* <= max(1e-6, 4 x the reference's own 1e-15-perturbation
+  spread); where the reference's step sequence is stable under that perturbation, the inner
+  iteration counts and EVERY accepted step size must be identical;
+* truncated n=8192 runs (M3-QP phase 1, M3-QP barrier phase from x_f, M3-LP): the first K Newton
+  steps' step sizes identical, Newton decrements within 1e-6 relative, the iterate after K steps
+  within 1e-6 relative;
+* M5 (SOCP n=4096, 256 cones): the reference's own FunctionManagerSOCP caches 2 K n^2 doubles
+  (64 GiB), so it is checked against the oracle's stacked-cone restatement (pinned to the
+  reference by the small SOCP fixtures): the first Newton steps' sizes identical, x within 1e-6.
+"""
+import ast
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+XSTAR_RTOL = 1e-6
+ND_RTOL = 1e-6
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _fixture(name):
+    path = os.path.join(GOLDEN, name + ".npz")
+    if not os.path.exists(path):
+        pytest.skip(f"fixture {name}.npz not generated")
+    return dict(np.load(path, allow_pickle=False))
+
+
+def _gram_on_device(Pp):
+    import torch
+    t = torch.as_tensor(Pp, device="cuda")
+    return (t.T @ t).cpu().numpy()
+
+
+def _instance(z):
+    """Regenerate the fixture's inputs from its generator spec and check the digest."""
+    from ipm355 import problems
+    spec = ast.literal_eval(str(z["spec"]))
+    if spec["gen"] == "qp_ineq_box":
+        inst = problems.qp_ineq_box(spec["n"], spec["m"], seed=spec["seed"], grid=spec["grid"], with_xf=True,
+                                    gram=_gram_on_device)
+    else:
+        inst = problems.lp_ineq_box(spec["n"], spec["m"], seed=spec["seed"], grid=spec["grid"], with_xf=True)
+    xf = inst.pop("xf")
+    assert problems.input_digest(inst) == str(z["digest"]), "regenerated inputs differ from the reference's"
+    kw = ast.literal_eval(str(z["kwargs"]))
+    kw.pop("x0", None)
+    if spec.get("x0") == "xf":
+        kw["x0"] = xf
+    return spec, dict(inst, **kw)
+
+
+def _cls(spec):
+    import ipm355
+    return ipm355.QPSolver if spec["gen"] == "qp_ineq_box" else ipm355.LPSolver
+
+
+def _device_trace(s):
+    p1 = getattr(s, "phase1_solver", None)
+    tr = (list(p1.phase1_ns.trace) if p1 is not None else []) + list(s.ns.trace)
+    return np.array([t[0] for t in tr]), np.array([t[1] for t in tr])
+
+
+def _check_full(name):
+    z = _fixture(name)
+    spec, kw = _instance(z)
+    s = _cls(spec)(check_cvxpy=False, suppress_print=True, **kw)
+    np.testing.assert_array_equal(np.asarray(s.x), z["x_init"])
+    v = s.solve()
+    err = rel(s.xstar, z["xstar"])
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    steps, nds = _device_trace(s)
+    print(f"[{name}] x* rel {err:.2e} (tol {xtol:.1e}), value {v!r} vs {float(z['value'])!r}, "
+          f"{len(steps)} Newton steps (reference {len(z['trace_step'])}), iters {list(s.inner_iters)}")
+    assert err <= xtol, err
+    assert abs(v - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * max(1.0, abs(float(z["value"])))
+    if bool(z["sens_steps_stable"]):
+        assert list(s.inner_iters) == list(z["inner_iters"])
+        assert list(s.phase1_solver.inner_iters if s.phase1_solver is not None else []) == \
+            list(z["phase1_inner_iters"])
+        np.testing.assert_array_equal(steps, z["trace_step"])
+        nd_err = np.abs(nds - z["trace_nd"]) / np.maximum(np.abs(z["trace_nd"]), 1e-300)
+        assert nd_err.max() <= ND_RTOL, nd_err.max()
+    return s
+
+
+def test_m2_qp_full_solve():
+    """M2: QP n=2048, m=512, test_QP kwargs, phase 1 + 10 barrier centering steps (881 Newton steps)."""
+    _check_full("m2_qp")
+
+
+@pytest.mark.parametrize("name", ["m3_qp_ph1", "m3_qp_feas", "m3_lp"])
+def test_m3_truncated_trajectory(name):
+    """M3 at n=8192, m=2048: the first K Newton steps of the headline QP (phase 1, then from x_f the
+    barrier phase) and of the LP, against the reference's steps, decrements and iterate."""
+    z = _fixture(name)
+    spec, kw = _instance(z)
+    K = int(z["k_steps"])
+    s = _cls(spec)(check_cvxpy=False, suppress_print=True, **kw)
+    np.testing.assert_array_equal(np.asarray(s.x), z["x_init"])
+    s.solve(iteration_budget=K)
+    steps, nds = _device_trace(s)
+    xk_ref = z["x_k"]
+    if len(xk_ref) == spec["n"] + 1:
+        xk = s.phase1_solver.x.cpu().numpy()
+    else:
+        xk = s.x_last.cpu().numpy()
+    err = rel(xk, xk_ref)
+    nd_err = np.abs(nds - z["trace_nd"]) / np.maximum(np.abs(z["trace_nd"]), 1e-300)
+    print(f"[{name}] K={K}: x_K rel {err:.2e}, nd max rel {nd_err.max():.2e}, steps equal "
+          f"{np.array_equal(steps, z['trace_step'])}, reference stable {bool(z['sens_steps_stable'])}")
+    assert len(steps) == K
+    assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xk_rel"])), err
+    if bool(z["sens_steps_stable"]):
+        np.testing.assert_array_equal(steps, z["trace_step"])
+        assert nd_err.max() <= ND_RTOL, nd_err.max()
+
+
+def test_m4_shard_on_one_gpu():
+    """Config 4 shard: eight of the 64 M4 instances (seeds 1000..1007, n=2048, m=512) solved by the
+    sharded driver (ipm355.dist.solve_sharded, world 1 -> every instance on this GPU), x* gathered
+    through the same table the multi-GPU run all_gathers, each against its reference fixture."""
+    from ipm355 import dist
+    from ipm355 import QPSolver
+    names = [f"m4_qp_{sd}" for sd in range(1000, 1008)]
+    zs = [_fixture(nm) for nm in names]
+    insts = [_instance(z)[1] for z in zs]
+    tab, X = dist.solve_sharded(lambda i: {k: v for k, v in insts[i].items()}, len(insts), QPSolver,
+                                device=0, gather_x=True)
+    for i, z in enumerate(zs):
+        err = rel(X[i], z["xstar"])
+        ref_iters = int(sum(z["inner_iters"]) + sum(z["phase1_inner_iters"]))
+        print(f"[{names[i]}] x* rel {err:.2e}, value {tab[i, 0]!r} vs {float(z['value'])!r}, "
+              f"iters {int(tab[i, 1])} vs {ref_iters}")
+        assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"])), (names[i], err)
+        assert abs(tab[i, 0] - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * abs(float(z["value"]))
+        if bool(z["sens_steps_stable"]):
+            assert int(tab[i, 1]) == ref_iters
+
+
+def test_m5_socp_against_oracle():
+    """M5: SOCPSolver n=4096, K=256 cones of 16 rows, P=I, strictly feasible x0 (phase 1 skipped):
+    the first centering step truncated to 3 Newton steps on the device and in the oracle."""
+    import ipm355
+    from ipm355 import problems
+    from oracle import ipm_oracle as O
+    inst = problems.socp_cones(n=4096, K=256, mi=16, seed=0)
+    x0 = inst.pop("x0")
+    kw = dict(problems.SOCP_KWARGS, max_outer_iters=1, max_inner_iters=3)
+    g = ipm355.SOCPSolver(check_cvxpy=False, suppress_print=True, x0=x0.copy(), **inst, **kw)
+    g.solve()
+    c = O.SOCPSolver(x0=x0.copy(), **inst, **kw)
+    c.solve()
+    err = rel(g.xstar, c.xstar)
+    gs = [t[0] for t in g.ns.trace]
+    cs = [t["step"] for t in c.ns.trace]
+    print(f"[m5] x rel {err:.2e}, steps {gs} vs oracle {cs}, iters {list(g.inner_iters)} vs {list(c.inner_iters)}")
+    assert gs == cs
+    assert err <= XSTAR_RTOL
