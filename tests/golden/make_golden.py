@@ -65,7 +65,7 @@ def _pack_list(prefix, arrs, out):
 def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
     """Re-run the reference with one right-hand-side vector perturbed by 1e-15 (relative):
     the spread of x*, value and iteration counts is the reference's own numerical envelope."""
-    key = next(k for k in ("b", "g", "d", "q") if isinstance(kwargs.get(k), np.ndarray))
+    key = next(k for k in ("b", "g", "d", "q", "c") if isinstance(kwargs.get(k), np.ndarray))
     rng = np.random.default_rng(1234)
     wx = wv = 0.0
     stable = True
@@ -218,7 +218,6 @@ def group_lasso():
 
 
 def main():
-    _wrap_feasible()
     fm_kats()
     run_solve("lp_eq_box", RefLP, dict(problems.lp_eq_box(200, 50, seed=0), update_slacks_every=5))
     run_solve("lp_ineq_box", RefLP, problems.lp_ineq_box(200, 50, seed=0))
@@ -252,5 +251,52 @@ def main():
     group_lasso()
 
 
+def eq_box_stable():
+    """Diagonal infeasible-start class (NewtonSolverCholeskyDiagonalInfeasibleStart) on trajectories
+    the reference itself keeps stable: lp_eq_box with the LPSolver defaults (epsilon 1e-10) drives t
+    to ~1e12 where its own x* moves 1e-4 under a 1e-15 input perturbation; with the test_LP kwargs
+    (testSolver.py:130-148) the spread is ~1e-9 and the iteration counts are stable."""
+    for sd in (1, 2):
+        run_solve(f"lp_eq_box_tk{sd}", RefLP, dict(problems.lp_eq_box(200, 50, seed=sd), **problems.LP_KWARGS))
+    run_solve("lp_eq_box_tk1_us5", RefLP, dict(problems.lp_eq_box(200, 50, seed=1), **problems.LP_KWARGS,
+                                               update_slacks_every=5))
+
+
+def extra():
+    """Round-2 fixtures: the remaining solve classes pinned by the reference itself."""
+    # feasible NewtonSolverDiagonal: LP with bounds only, no C, no A (LPSolver.py:436-446 dispatch)
+    rng = np.random.default_rng(11)
+    n = 300
+    run_solve("lp_box_diag", RefLP, dict(c=rng.uniform(-2, 2, n), lower_bound=-1.0, upper_bound=2.0))
+    rng = np.random.default_rng(12)
+    lb = rng.uniform(-2, 0, n)
+    ub = lb + rng.uniform(0.5, 3, n)
+    run_solve("lp_box_diag_vec", RefLP, dict(c=rng.normal(size=n), lower_bound=lb, upper_bound=ub,
+                                             **problems.LP_KWARGS))
+    eq_box_stable()
+    # linear_solve_method np_solve / np_lstsq / direct on the dense classes (NewtonSolver.py:212-361,
+    # NewtonSolverInfeasibleStart.py:279-354, 541-755)
+    for meth in ("np_solve", "np_lstsq", "direct"):
+        run_solve(f"meth_qp_ineq_box_{meth}", RefQP, dict(problems.qp_ineq_box(128, 32, seed=1), **problems.QP_KWARGS,
+                                                          linear_solve_method=meth))
+        rng = np.random.default_rng(5)
+        n = 60
+        C = rng.random((25, n)) * rng.binomial(1, 0.3, (25, n))
+        d = rng.integers(1, 30, 25).astype(float)
+        c = rng.integers(1, n, n) - n / 2
+        Aeq = np.hstack((1, np.zeros(n - 1))).reshape(1, -1)
+        run_solve(f"meth_qp_eq_phase1_{meth}", RefQP, dict(P=np.eye(n), q=c, A=Aeq, b=np.array([1.0]), C=C, d=d,
+                                                          t0=0.1, upper_bound=None, lower_bound=0, mu=15,
+                                                          x0=np.ones(n) * 10, linear_solve_method=meth))
+        run_solve(f"meth_lp_ineq_box_{meth}", RefLP, dict(problems.lp_ineq_box(128, 32, seed=3), **problems.LP_KWARGS,
+                                                          linear_solve_method=meth))
+
+
 if __name__ == "__main__":
-    main()
+    _wrap_feasible()
+    if sys.argv[1:] == ["extra"]:
+        extra()
+    elif sys.argv[1:] == ["eq_box_stable"]:
+        eq_box_stable()
+    else:
+        main()

@@ -10,11 +10,19 @@ SOLVE_CASES = {
     "lp_eq_box": "LP", "lp_ineq_box": "LP", "lp_ineq_box_testkw": "LP", "lp_eq_ineq": "LP",
     "qp_ineq_box": "QP", "qp_ineq_box_256": "QP", "qp_feasible": "QP", "qp_eq_phase1": "QP",
     "socp_small": "SOCP", "socp_small_eq": "SOCP", "socp_phase1": "SOCP", "socp_group_lasso": "SOCP",
+    # round 2: feasible NewtonSolverDiagonal (bounds only) and stable diagonal infeasible-start runs
+    "lp_box_diag": "LP", "lp_box_diag_vec": "LP",
+    "lp_eq_box_tk1": "LP", "lp_eq_box_tk2": "LP", "lp_eq_box_tk1_us5": "LP",
 }
+
+# linear_solve_method np_solve / np_lstsq / direct, pinned by the reference (make_golden.py extra)
+METHOD_CASES = {f"meth_{case}_{meth}": kind
+                for case, kind in (("qp_ineq_box", "QP"), ("qp_eq_phase1", "QP"), ("lp_ineq_box", "LP"))
+                for meth in ("np_solve", "np_lstsq", "direct")}
 
 # kwargs that are stored as scalars in the fixture but are not array inputs
 _SCALAR_KW = {"t0", "mu", "epsilon", "alpha", "beta", "max_inner_iters", "max_outer_iters",
-              "update_slacks_every", "lower_bound", "upper_bound"}
+              "update_slacks_every", "lower_bound", "upper_bound", "linear_solve_method"}
 
 
 def load(name):

@@ -27,7 +27,14 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 XSTAR_RTOL = 1e-6
-ND_RTOL = 1e-6
+# Newton decrement nd = -g.dx/2: relative 1e-6, plus an absolute 1e-9 for the steps where nd has
+# cancelled down to ~1e-8 (end of a centering step; g and dx are O(1e2..1e4) there)
+ND_RTOL, ND_ATOL = 1e-6, 1e-9
+
+
+def nd_excess(nds, ref):
+    """max over steps of |nd - nd_ref| / (ND_RTOL |nd_ref| + ND_ATOL); <= 1 passes"""
+    return float(np.max(np.abs(nds - ref) / (ND_RTOL * np.abs(ref) + ND_ATOL))) if len(ref) else 0.0
 
 
 def rel(a, b):
@@ -95,8 +102,7 @@ def _check_full(name):
         assert list(s.phase1_solver.inner_iters if s.phase1_solver is not None else []) == \
             list(z["phase1_inner_iters"])
         np.testing.assert_array_equal(steps, z["trace_step"])
-        nd_err = np.abs(nds - z["trace_nd"]) / np.maximum(np.abs(z["trace_nd"]), 1e-300)
-        assert nd_err.max() <= ND_RTOL, nd_err.max()
+        assert nd_excess(nds, z["trace_nd"]) <= 1.0, nd_excess(nds, z["trace_nd"])
     return s
 
 
@@ -122,14 +128,14 @@ def test_m3_truncated_trajectory(name):
     else:
         xk = s.x_last.cpu().numpy()
     err = rel(xk, xk_ref)
-    nd_err = np.abs(nds - z["trace_nd"]) / np.maximum(np.abs(z["trace_nd"]), 1e-300)
-    print(f"[{name}] K={K}: x_K rel {err:.2e}, nd max rel {nd_err.max():.2e}, steps equal "
+    nd_x = nd_excess(nds, z["trace_nd"]) if len(nds) == len(z["trace_nd"]) else float("inf")
+    print(f"[{name}] K={K}: x_K rel {err:.2e}, nd excess {nd_x:.2e}, steps equal "
           f"{np.array_equal(steps, z['trace_step'])}, reference stable {bool(z['sens_steps_stable'])}")
     assert len(steps) == K
     assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xk_rel"])), err
     if bool(z["sens_steps_stable"]):
         np.testing.assert_array_equal(steps, z["trace_step"])
-        assert nd_err.max() <= ND_RTOL, nd_err.max()
+        assert nd_x <= 1.0, nd_x
 
 
 def test_m4_shard_on_one_gpu():

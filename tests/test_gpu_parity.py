@@ -17,7 +17,7 @@ trajectories rather than average them").
 import numpy as np
 import pytest
 
-from golden_io import SOLVE_CASES, load, solver_kwargs
+from golden_io import METHOD_CASES, SOLVE_CASES, load, solver_kwargs
 
 pytestmark = pytest.mark.gpu
 
@@ -95,7 +95,8 @@ def _run(name):
     kw["x0"] = z["x_init"].copy()
     kw["check_cvxpy"] = False
     kw["suppress_print"] = True
-    cls = {"LP": ipm355.LPSolver, "QP": ipm355.QPSolver, "SOCP": ipm355.SOCPSolver}[SOLVE_CASES[name]]
+    kind = {**SOLVE_CASES, **METHOD_CASES}[name]
+    cls = {"LP": ipm355.LPSolver, "QP": ipm355.QPSolver, "SOCP": ipm355.SOCPSolver}[kind]
     s = cls(**kw)
     v = s.solve()
     return z, s, v
@@ -236,3 +237,23 @@ def test_other_linear_solve_methods(name, method):
         return
     assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"])), (err,)
     assert abs(v - vc) <= max(1e-8, 4 * float(z["sens_value_rel"])) * max(1.0, abs(vc))
+
+
+@pytest.mark.parametrize("name", sorted(METHOD_CASES))
+def test_linear_solve_methods_vs_reference(name):
+    """linear_solve_method np_solve / np_lstsq / direct against fixtures the REFERENCE produced
+    (make_golden.py extra; NewtonSolver.py:212-361, NewtonSolverInfeasibleStart.py:279-354, 541-755):
+    same bar as the cholesky full solves -- x* within max(1e-6, 4 x the reference's own spread), and
+    where the reference's iteration counts are stable under a 1e-15 perturbation, identical counts
+    and step sequences."""
+    z, s, v = _run(name)
+    err = rel(s.xstar, z["xstar"])
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    print(f"[{name}] x* rel {err:.1e} (tol {xtol:.1e}), iters {list(s.inner_iters)} vs {list(z['inner_iters'])}")
+    assert err <= xtol, err
+    assert abs(v - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * max(1.0, abs(float(z["value"])))
+    if bool(z["sens_iters_stable"]):
+        assert list(s.inner_iters) == list(z["inner_iters"])
+        steps = [t[0] for t in ((s.phase1_solver.phase1_ns.trace if len(z["phase1_inner_iters"]) else [])
+                                + s.ns.trace)]
+        np.testing.assert_array_equal(np.array(steps), z["trace_step"])

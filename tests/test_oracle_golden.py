@@ -10,7 +10,7 @@ container (tests/golden/make_golden.py).  The oracle must reproduce:
 import numpy as np
 import pytest
 
-from golden_io import SOLVE_CASES, load, solver_kwargs
+from golden_io import METHOD_CASES, SOLVE_CASES, load, solver_kwargs
 from oracle import ipm_oracle as O
 
 
@@ -96,12 +96,12 @@ def oracle_solver(kind, kw):
     return cls(**kw)
 
 
-@pytest.mark.parametrize("name", sorted(SOLVE_CASES))
+@pytest.mark.parametrize("name", sorted(SOLVE_CASES) + sorted(METHOD_CASES))
 def test_full_solve_matches_reference(name):
     z = load(name)
     kw = solver_kwargs(z)
     kw["x0"] = z["x_init"].copy()
-    s = oracle_solver(SOLVE_CASES[name], kw)
+    s = oracle_solver({**SOLVE_CASES, **METHOD_CASES}[name], kw)
     val = s.solve()
     steps = [tr["step"] for tr in (s.phase1.ns.trace if s.phase1_iters else [])] + [tr["step"] for tr in s.ns.trace]
     assert list(s.inner_iters) == list(z["inner_iters"])
