@@ -148,18 +148,21 @@ def make(case):
     key = "d"
     rng = np.random.default_rng(1234)
     wx, wv, stable, wk = 0.0, 0.0, True, 0.0
+    wnd = np.zeros(len(base["nds"]))
     for _ in range(1 if (limit is not None or case.startswith("m4_")) else 2):
         kp = dict(kw)
         kp[key] = kw[key] * (1 + 1e-15 * rng.standard_normal(kw[key].shape))
         r = run_once(cls, kp, limit)
         stable &= r["steps"] == base["steps"]
-        if limit is None:
+        if len(r["nds"]) == len(base["nds"]):      # per-step spread of the Newton decrement
+            b = np.array(base["nds"])
+            wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))        if limit is None:
             wx = max(wx, float(np.linalg.norm(r["xstar"] - base["xstar"]) / np.linalg.norm(base["xstar"])))
             wv = max(wv, abs(r["value"] - base["value"]) / max(abs(base["value"]), 1e-300))
         elif r["x_limit"] is not None and base["x_limit"] is not None and r["x_limit"].shape == base["x_limit"].shape:
             wk = max(wk, float(np.linalg.norm(r["x_limit"] - base["x_limit"]) / np.linalg.norm(base["x_limit"])))
     out.update(sens_key=np.array(key), sens_xstar_rel=np.array(wx), sens_value_rel=np.array(wv),
-               sens_xk_rel=np.array(wk), sens_steps_stable=np.array(stable))
+               sens_xk_rel=np.array(wk), sens_steps_stable=np.array(stable), sens_nd_rel=wnd)
     np.savez_compressed(os.path.join(HERE, case + ".npz"), **out)
     print(f"{case}: {el:.0f}s steps={len(base['steps'])} (phase1 {sum(base['ph1'])}) inner={base['inner_iters']} "
           f"ph1 inner={base['phase1_inner_iters']} value={base['value']} stable={stable} "

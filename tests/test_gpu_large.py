@@ -32,9 +32,18 @@ XSTAR_RTOL = 1e-6
 ND_RTOL, ND_ATOL = 1e-6, 1e-9
 
 
-def nd_excess(nds, ref):
-    """max over steps of |nd - nd_ref| / (ND_RTOL |nd_ref| + ND_ATOL); <= 1 passes"""
-    return float(np.max(np.abs(nds - ref) / (ND_RTOL * np.abs(ref) + ND_ATOL))) if len(ref) else 0.0
+def nd_excess(nds, ref, spread=None):
+    """max over steps of |nd - nd_ref| / ((max(ND_RTOL, 4 spread_k)) |nd_ref| + ND_ATOL); <= 1 passes.
+    spread_k = the reference's own relative change of nd at step k under the 1e-15 input
+    perturbation: in the stuck centering steps at large t (Q1) H is so ill-conditioned that the
+    reference itself moves nd by ~1e-5 there."""
+    if not len(ref):
+        return 0.0
+    rt = ND_RTOL if spread is None else np.maximum(ND_RTOL, 4 * spread)
+    e = np.abs(nds - ref) / (rt * np.abs(ref) + ND_ATOL)
+    for i in np.argsort(e)[::-1][:4]:
+        print(f"    nd step {i}: device {nds[i]!r} reference {ref[i]!r} excess {e[i]:.2f}")
+    return float(e.max())
 
 
 def rel(a, b):
@@ -102,7 +111,8 @@ def _check_full(name):
         assert list(s.phase1_solver.inner_iters if s.phase1_solver is not None else []) == \
             list(z["phase1_inner_iters"])
         np.testing.assert_array_equal(steps, z["trace_step"])
-        assert nd_excess(nds, z["trace_nd"]) <= 1.0, nd_excess(nds, z["trace_nd"])
+        ndx = nd_excess(nds, z["trace_nd"], z.get("sens_nd_rel"))
+        assert ndx <= 1.0, ndx
     return s
 
 
@@ -128,7 +138,7 @@ def test_m3_truncated_trajectory(name):
     else:
         xk = s.x_last.cpu().numpy()
     err = rel(xk, xk_ref)
-    nd_x = nd_excess(nds, z["trace_nd"]) if len(nds) == len(z["trace_nd"]) else float("inf")
+    nd_x = nd_excess(nds, z["trace_nd"], z.get("sens_nd_rel")) if len(nds) == len(z["trace_nd"]) else float("inf")
     print(f"[{name}] K={K}: x_K rel {err:.2e}, nd excess {nd_x:.2e}, steps equal "
           f"{np.array_equal(steps, z['trace_step'])}, reference stable {bool(z['sens_steps_stable'])}")
     assert len(steps) == K
