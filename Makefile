@@ -10,9 +10,9 @@ OBJ_DIR  := build/obj
 # dot products and MFMA use explicit fma where intended.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-result -Wno-unused-value -Iinclude -I$(SRC_DIR)
-SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip
+SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip $(SRC_DIR)/ipm_lasso.hip
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
-HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h include/ipm355.h
+HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
 
 all: $(OUT)
 
@@ -31,7 +31,7 @@ $(TRACE_OUT): $(SRCS) $(HDRS)
 	@mkdir -p build/trace
 	$(HIPCC) $(HIPFLAGS) -DIPM_ROLE_TRACE -c $(SRC_DIR)/ipm_blas.hip -o build/trace/ipm_blas.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC build/trace/ipm_blas.o $(OBJ_DIR)/ipm_barrier.o \
-	    $(OBJ_DIR)/ipm_engine.o -o $@
+	    $(OBJ_DIR)/ipm_engine.o $(OBJ_DIR)/ipm_lasso.o -o $@
 
 clean:
 	rm -rf build $(OUT)

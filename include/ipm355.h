@@ -194,6 +194,68 @@ int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* co
    the CUs the panel chain leaves idle (opt-in, IPM_DEFER=1) */
 int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred);
 
+/* ---- batched ADMM Lasso (LassoSolver.py) ------------------------------ *
+ * S problems  min_x 1/(2m) ||A x - b_s||^2 + reg_s ||x||_1  solved together.  Every n x S matrix
+ * below is row-major with leading dimension lds (element (i, s) at i*lds + s).                  */
+typedef struct ipm_lasso_args {
+  int64_t n, S, m;         /* variables (incl. the bias column), problems, rows of A           */
+  int64_t lds;             /* leading dimension of x, alpha, u, W0, W1                         */
+  const double* Qs;        /* [dev] n x n, ldq: (-m rho Q)^T, Q = (diag(m rho) + A^T A)^-1      */
+  int64_t ldq;
+  const double* bA;        /* [dev] n x (S or 1), ldba: Q A^T b (LassoSolver.py:214-219)         */
+  int64_t ldba;
+  const double* eta;       /* [dev] S or 1: reg / rho                                         */
+  double* x;               /* [dev] state (zeros on entry, LassoSolver.py:222-236)             */
+  double* alpha;
+  double* u;
+  double* W0;              /* [dev] u - alpha on entry; W1 scratch (ping-pong)                 */
+  double* W1;
+  double* partial;         /* [dev] >= ipm_lasso_partial_doubles(n, S)                         */
+  double rho, eps_abs, eps_rel, stop_multiplier;
+  int32_t max_iters, check_stop;
+  int32_t positive, add_bias;
+  int32_t dual_form;       /* 0: u = u + x - alpha (:251); 1: u = u + (x - alpha) (chunks, :413) */
+  int32_t compute_loss;    /* per-iteration loss into gaps (LassoSolver.py:254-268)            */
+  int32_t ba_bcast, eta_bcast, b_bcast, reg_bcast;   /* 1: a single column / value for all S   */
+  /* loss evaluation (compute_loss, ipm_lasso_loss) */
+  const double* AT;        /* [dev] n x m, ldat: A^T row-major                                 */
+  int64_t ldat;
+  const double* b;         /* [dev] m x (S or 1), ldb                                          */
+  int64_t ldb;
+  const double* reg;       /* [dev] S or 1                                                    */
+  double* R;               /* [dev] m x S scratch                                             */
+  double* gaps;            /* [dev] max_iters rows of ldg: gaps[it*ldg + col(s)]               */
+  int64_t ldg;
+  const int64_t* gap_cols; /* [dev] S: column of problem s in gaps (chunks), NULL: s            */
+} ipm_lasso_args;
+
+/* row-major C (M x N, ldc) = alpha A^T B + beta C; A: K x M (lda), B: K x N (ldb); fp64 MFMA */
+int ipm_gemm_tn(ipm_handle* h, int64_t M, int64_t N, int64_t K, double alpha, const double* A, int64_t lda,
+                const double* B, int64_t ldb, double beta, double* C, int64_t ldc);
+/* out (cols x rows, ldo) = in^T (rows x cols, ldi), row-major; device copy of n doubles */
+int ipm_transpose(ipm_handle* h, int64_t rows, int64_t cols, const double* in, int64_t ldi, double* out,
+                  int64_t ldo);
+int ipm_copy(ipm_handle* h, double* dst, const double* src, int64_t n);
+/* normalize_A (LassoSolver.py:122-123): A /= A.std(axis=0) in place; stdv [dev] n (may be NULL) */
+int ipm_lasso_colnorm(ipm_handle* h, int64_t m, int64_t n, double* A, int64_t lda, double* stdv);
+/* add_bias (LassoSolver.py:124-131): out (m x (n+1), ldo) = [1 | A] */
+int ipm_lasso_bias(ipm_handle* h, int64_t m, int64_t n, const double* A, int64_t lda, double* out, int64_t ldo);
+/* LassoSolver.py:157-189: Q = (diag(m rho) + A^T A)^-1 via Cholesky (info as ipm_potrf), QT = Q^T */
+int ipm_lasso_qinv(ipm_handle* h, int64_t m, int64_t n, const double* A, int64_t lda, double rho, double* Q,
+                   double* QT, int64_t ldq, int* info);
+/* M (rows x cols, ld) *= f1 (then *= f2 when two): Qinv *= -m*rho, or Qinv * -m * rho (chunks) */
+int ipm_lasso_scale(ipm_handle* h, int64_t rows, int64_t cols, double* M, int64_t ld, double f1, double f2,
+                    int two);
+/* prox (LassoSolver.py:533-558): out = soft-threshold(v, eta), row 0 kept with add_bias */
+int ipm_lasso_prox(ipm_handle* h, int64_t n, int64_t S, const double* v, int64_t ldv, const double* eta,
+                   int eta_bcast, int positive, int add_bias, double* out, int64_t ldo);
+/* loss per problem of the current alpha into out[cols ? cols[s] : s]; absm: |alpha| in the l1 term */
+int ipm_lasso_loss(ipm_handle* h, const ipm_lasso_args* a, int absm, double* out, const int64_t* cols);
+int64_t ipm_lasso_partial_doubles(int64_t n, int64_t S);
+/* the ADMM loop (LassoSolver.py:240-337, one chunk of :339-485): iterates until the stopping
+   test (every check_stop iterations) or max_iters; *iters = the last iteration index */
+int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* iters);
+
 #ifdef __cplusplus
 }
 #endif

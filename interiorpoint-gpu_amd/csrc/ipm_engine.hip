@@ -25,6 +25,7 @@
 #include "../../include/ipm355.h"
 #include "ipm_barrier.h"
 #include "ipm_common.h"
+#include "ipm_handle.h"
 
 using namespace ipm;
 
@@ -33,7 +34,7 @@ constexpr double STEP_FLOOR = 1e-13;  // NewtonSolver.py:176, 190
 constexpr int NCAND = 64;
 // readback block layout (bytes): info (8 ints), mask (4 words), sums (NCAND), scal (64)
 constexpr int RB_MASK = 32, RB_SUMS = 64, RB_SCAL = RB_SUMS + NCAND * 8;
-constexpr int HOST_WORDS = 4096;
+constexpr int HOST_WORDS = IPM_HOST_WORDS;
 
 enum Slot {
   SC_F0A = 0,  // c.x | x.Px | s
@@ -53,35 +54,6 @@ enum Slot {
   SC_COUNT
 };
 }  // namespace
-
-struct ipm_handle {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  PotrfStreams pst;                  // Cholesky look-ahead: panel / trailing streams (CU-masked)
-  bool own_stream = false;
-  std::string err;
-  double* hbuf = nullptr;  // pinned host staging
-  int* dinfo = nullptr;    // device scratch for level-0 potrf
-  unsigned* ctl = nullptr; // device control words for level-0 potrs
-  double* pws = nullptr;   // device workspace for level-0 potrf (grown on demand)
-  int64_t pws_n = 0;
-  double* scratch = nullptr;
-  size_t scratch_bytes = 0;
-  hipEvent_t ev[6];
-  double kkt_sum = 0.0, potrf_sum = 0.0;
-  int64_t kkt_cnt = 0, potrf_cnt = 0;
-  bool timing = false;
-  bool kkt_pending = false, potrf_pending = false;
-};
-
-#define HIPCHK(h, expr)                                                        \
-  do {                                                                         \
-    hipError_t _e = (expr);                                                    \
-    if (_e != hipSuccess) {                                                    \
-      (h)->err = std::string(#expr) + ": " + hipGetErrorString(_e);            \
-      return IPM_HIP_ERROR;                                                    \
-    }                                                                          \
-  } while (0)
 
 struct ipm_problem {
   ipm_handle* h = nullptr;
@@ -517,16 +489,7 @@ extern "C" int ipm_destroy(ipm_handle* h) {
 
 extern "C" const char* ipm_last_error(ipm_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
-static double* scratch(ipm_handle* h, size_t bytes) {
-  if (bytes > h->scratch_bytes) {
-    if (h->scratch) hipFree(h->scratch);
-    h->scratch = nullptr;
-    h->scratch_bytes = 0;
-    if (hipMalloc((void**)&h->scratch, bytes) != hipSuccess) return nullptr;
-    h->scratch_bytes = bytes;
-  }
-  return h->scratch;
-}
+static double* scratch(ipm_handle* h, size_t bytes) { return ipm_handle_scratch(h, bytes); }
 
 // ======================================================================= level 0
 extern "C" int ipm_gemv(ipm_handle* h, int trans, int64_t rows, int64_t cols, double alpha, const double* M,

@@ -85,6 +85,18 @@ EXPORTS = {
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),
+    # batched ADMM Lasso (ipm_lasso.hip; ipm355/lasso.py)
+    "ipm_gemm_tn": (C.c_int, [P, I64, I64, I64, F64, P, I64, P, I64, F64, P, I64]),
+    "ipm_transpose": (C.c_int, [P, I64, I64, P, I64, P, I64]),
+    "ipm_copy": (C.c_int, [P, P, P, I64]),
+    "ipm_lasso_colnorm": (C.c_int, [P, I64, I64, P, I64, P]),
+    "ipm_lasso_bias": (C.c_int, [P, I64, I64, P, I64, P, I64]),
+    "ipm_lasso_qinv": (C.c_int, [P, I64, I64, P, I64, F64, P, P, I64, C.POINTER(C.c_int)]),
+    "ipm_lasso_scale": (C.c_int, [P, I64, I64, P, I64, F64, F64, C.c_int]),
+    "ipm_lasso_prox": (C.c_int, [P, I64, I64, P, I64, P, C.c_int, C.c_int, C.c_int, P, I64]),
+    "ipm_lasso_loss": (C.c_int, [P, P, C.c_int, P, P]),
+    "ipm_lasso_partial_doubles": (I64, [I64, I64]),
+    "ipm_lasso_admm": (C.c_int, [P, P, C.POINTER(C.c_int32)]),
 }
 
 _lib = None

@@ -107,6 +107,55 @@ def socp_cones(n=4096, K=256, mi=16, seed=0, eq=0):
     return out
 
 
+def _g(a):
+    """round to multiples of 2^-10 (products and the dot products below stay exact in fp64)"""
+    return np.round(a / GRID) * GRID
+
+
+LASSO_CASES = ("lasso_demo", "lasso_regpath", "lasso_positive", "lasso_chunks", "lasso_testsolver", "lasso_n1024")
+
+
+def lasso_instance(name):
+    """LassoSolver instances in the reference's own usage patterns -> (A, b, reg, kwargs).
+
+    demo.ipynb cells 47-48 (m=500, n=150, 30 problems, bias, normalised A, loss tracked; positive and
+    chunked variants), cells 53-54 (one b, 50 regularisation strengths), testSolver.py:1057-1160
+    (test_Lasso: rows = 3 x 0.8 n, 30 problems, reg = 0.05 + 0.01 N).  Values sit on the 2^-10 grid so
+    that b = A x_true + noise is exact whatever BLAS computes it (the GPU box regenerates the inputs
+    bit for bit; the fixtures store only their digest)."""
+    rng = np.random.default_rng(dict(zip(LASSO_CASES, range(7, 7 + len(LASSO_CASES))))[name])
+    base = dict(rho=0.4, max_iters=1000, check_stop=10, add_bias=True, normalize_A=False, positive=False,
+                compute_loss=False, adaptive_rho=False, eps_abs=1e-6, eps_rel=1e-6, use_gpu=False, num_chunks=0,
+                check_cvxpy=False)
+
+    def sparse_x(n, S, nnz):
+        xt = np.zeros((n, S))
+        xt[np.unravel_index(rng.integers(0, n * S, nnz), (n, S))] = _g(rng.uniform(0, 50, nnz))
+        return xt
+    if name in ("lasso_demo", "lasso_positive", "lasso_chunks"):
+        m, n, S = 500, 150, 30
+        A = _g(rng.random((m, n)))
+        b = A @ sparse_x(n, S, 1000) + _g(rng.standard_normal((m, S)))
+        reg = 0.05 + 0.01 * rng.standard_normal(S)
+        kw = dict(base, normalize_A=True, compute_loss=True, eps_rel=1e-4)
+        if name == "lasso_positive":
+            kw.update(positive=True, compute_loss=False, eps_abs=1e-4, eps_rel=3e-2, check_stop=5)
+        if name == "lasso_chunks":
+            kw.update(num_chunks=3, normalize_A=False)
+        return A, b, reg, kw
+    if name == "lasso_regpath":
+        m, n = 800, 400
+        A = _g(rng.random((m, n)))
+        b = A @ sparse_x(n, 1, 10000) + _g(rng.standard_normal((m, 1)))
+        return A, b, np.logspace(-5, 2, 50), dict(base, rho=0.004, max_iters=3000, check_stop=100)
+    n = 400 if name == "lasso_testsolver" else 1024
+    rows, S = 3 * int(0.8 * n), 30
+    A = _g(rng.random((rows, n)))
+    b = A @ sparse_x(n, S, int(n * S / 4)) + _g(rng.standard_normal((rows, S)))
+    reg = 0.05 + 0.01 * rng.standard_normal(S)
+    return A, b, reg, dict(base, max_iters=1000 if name == "lasso_testsolver" else 400)
+
+
 def instance_seeds(total, rank, world):
     """M4 partitioning (SURVEY.md §8(e)): rank r takes instances r::world."""
     return list(range(rank, total, world))

@@ -19,8 +19,9 @@ never the inputs themselves (P alone is 512 MiB at n=8192)):
 Recorded per accepted Newton step: the returned backtracking step size and the Newton decrement
 nd = -g.dx/2 (both exactly what NewtonSolver.solve computes, NewtonSolver.py:93-133); for the
 truncated cases the iterate x_K after K steps (the x handed to the (K+1)-th line search).
-Sensitivity: one (truncated: one; full: two) re-run with the right-hand side perturbed by 1e-15
-relative gives the reference's own envelope and whether its step sequence is stable.
+Sensitivity (the reference's own envelope, and whether its step sequence is stable): re-runs with
+the right-hand side perturbed by 1e-15 relative (truncated and M4: one; M2: two), plus one re-run of
+the unperturbed inputs at 1 OpenBLAS thread (a different summation order in dpotrf).
 """
 from __future__ import annotations
 
@@ -47,6 +48,7 @@ from QPSolver import QPSolver as RefQP  # noqa: E402
 from ipm355 import problems  # noqa: E402
 
 K_TRUNC = int(os.environ.get("IPM_GOLDEN_K", "30"))
+ALT_THREADS = int(os.environ.get("IPM_GOLDEN_ALT_THREADS", "1"))
 
 
 class _StopK(Exception):
@@ -156,11 +158,29 @@ def make(case):
         stable &= r["steps"] == base["steps"]
         if len(r["nds"]) == len(base["nds"]):      # per-step spread of the Newton decrement
             b = np.array(base["nds"])
-            wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))        if limit is None:
+            wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))
+        if limit is None:
             wx = max(wx, float(np.linalg.norm(r["xstar"] - base["xstar"]) / np.linalg.norm(base["xstar"])))
             wv = max(wv, abs(r["value"] - base["value"]) / max(abs(base["value"]), 1e-300))
         elif r["x_limit"] is not None and base["x_limit"] is not None and r["x_limit"].shape == base["x_limit"].shape:
             wk = max(wk, float(np.linalg.norm(r["x_limit"] - base["x_limit"]) / np.linalg.norm(base["x_limit"])))
+    # ... and the reference's own spread under a different summation order: the unperturbed solve
+    # at 1 OpenBLAS thread (dpotrf's blocking depends on the thread count; a GPU factorization is
+    # just another summation order, so this is the envelope the Newton decrements are held to)
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=ALT_THREADS, user_api="blas"):
+        r = run_once(cls, kw, limit)
+    stable &= r["steps"] == base["steps"]
+    if len(r["nds"]) == len(base["nds"]):
+        b = np.array(base["nds"])
+        wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))
+    if limit is None:
+        wx = max(wx, float(np.linalg.norm(r["xstar"] - base["xstar"]) / np.linalg.norm(base["xstar"])))
+        wv = max(wv, abs(r["value"] - base["value"]) / max(abs(base["value"]), 1e-300))
+    elif r["x_limit"] is not None and base["x_limit"] is not None and r["x_limit"].shape == base["x_limit"].shape:
+        wk = max(wk, float(np.linalg.norm(r["x_limit"] - base["x_limit"]) / np.linalg.norm(base["x_limit"])))
+    out.update(sens_sources=np.array(f"{key} * (1 + 1e-15 N(0,1)); OpenBLAS {ALT_THREADS} thread(s) vs "
+                                     f"{os.environ['OPENBLAS_NUM_THREADS']}"))
     out.update(sens_key=np.array(key), sens_xstar_rel=np.array(wx), sens_value_rel=np.array(wv),
                sens_xk_rel=np.array(wk), sens_steps_stable=np.array(stable), sens_nd_rel=wnd)
     np.savez_compressed(os.path.join(HERE, case + ".npz"), **out)
