@@ -113,8 +113,15 @@ typedef struct ipm_newton_opts {
   double phase1_tol;
   double* trace;                 /* optional HOST buffer: per-iteration (step, stat) pairs  */
   int32_t trace_cap;             /* capacity in iterations (0: no trace)                   */
-  int32_t reserved;
+  int32_t linesearch_mode;       /* IPM_LS_* (feasible start)                                */
 } ipm_newton_opts;
+
+/* feasible-start backtracking (NewtonSolver.py:157-206) */
+#define IPM_LS_TABLE 0   /* 64 candidate steps per pass: slacks s0 + a ds, f(x + a dx) by its
+                            expansion; the reference's decision sequence replayed on the host   */
+#define IPM_LS_EXACT 1   /* reference-exact: every trial point formed, fresh d - C next_x slacks
+                            when the reference refreshes them, f(next_x) evaluated directly      */
+#define IPM_LS_COMPARE 2 /* both; the exact step is taken, disagreements counted (ls_flips)     */
 
 /* Result of one centering step: the tuple NewtonSolver.solve returns */
 typedef struct ipm_newton_result {
@@ -125,6 +132,8 @@ typedef struct ipm_newton_result {
   double stat;          /* nd = -g.dx/2 (feasible) or trial residual (infeasible)*/
   double last_step;     /* last accepted step size                               */
   int64_t backtracks;   /* total trial points examined                           */
+  int64_t ls_compared;  /* IPM_LS_COMPARE: steps compared / steps whose table and  */
+  int64_t ls_flips;     /*   exact step sizes differ                             */
 } ipm_newton_result;
 
 /* ---- handle --------------------------------------------------------------- */

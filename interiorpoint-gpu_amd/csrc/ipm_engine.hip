@@ -1084,49 +1084,125 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       }
       const double fx = t * f_at(pr, rb.sc, 0.0) - rb.sc[SC_SUMLOG0];
       const double gc = rb.sc[SC_GX];
-      // domain loop (NewtonSolver.py:172-183)
-      int64_t kd = -1, kstuck = -1;
-      for (int64_t k = 0;; ++k) {
-        tab.build(o->beta, k + 1);
-        if (k > 0 && tab.alpha[k] < STEP_FLOOR) { kstuck = k; break; }
-        if (k >= k0 + NCAND) {
-          k0 = k;
-          candidate_pass(pr, x, tab.alpha[k0], o->beta);
-          rc = readback(pr, rb, false);
-          if (rc) return rc;
+      // (a) the 64-candidate table: slacks s0 + a ds, f(x + a dx) from its expansion, decisions
+      //     replayed on the host (default)
+      auto table_step = [&](double* out) -> int {
+        int64_t kd = -1, kstuck = -1;
+        for (int64_t k = 0;; ++k) {
+          tab.build(o->beta, k + 1);
+          if (k > 0 && tab.alpha[k] < STEP_FLOOR) { kstuck = k; break; }
+          if (k >= k0 + NCAND) {
+            k0 = k;
+            candidate_pass(pr, x, tab.alpha[k0], o->beta);
+            const int rc2 = readback(pr, rb, false);
+            if (rc2) return rc2;
+          }
+          ++backtracks;
+          if (rb.mask & (1ull << (k - k0))) { kd = k; break; }
         }
-        ++backtracks;
-        if (rb.mask & (1ull << (k - k0))) { kd = k; break; }
-      }
-      double step;
-      if (kd < 0) {
-        step = tab.alpha[kstuck];
-      } else {
+        if (kd < 0) {
+          *out = tab.alpha[kstuck];
+          return IPM_OK;
+        }
         // Armijo loop with the reference's lag (Q3) and stale slacks (Q2)
         int64_t ks = kd, kx = kd, kslack = kd;
         int attempt = 0;
-        bool stuck = false;
         for (;;) {
           if (kslack < k0 || kslack >= k0 + NCAND) {
             k0 = kslack;
             tab.build(o->beta, k0 + NCAND);
             candidate_pass(pr, x, tab.alpha[k0], o->beta);
-            rc = readback(pr, rb, false);
-            if (rc) return rc;
+            const int rc2 = readback(pr, rb, false);
+            if (rc2) return rc2;
           }
           const double psi = t * f_at(pr, rb.sc, tab.alpha[kx]) - rb.sums[kslack - k0];
           if (!(psi > fx + o->alpha * tab.alpha[ks] * gc)) break;
           ++attempt;
           ++backtracks;
           const int64_t knext = ks;
-          if (tab.alpha[ks] < STEP_FLOOR) { stuck = true; break; }
+          if (tab.alpha[ks] < STEP_FLOOR) break;
           ++ks;
           tab.build(o->beta, ks + 1);
           kx = knext;
           if (K > 0 && attempt % K == K - 1) kslack = knext;
         }
-        (void)stuck;
-        step = tab.alpha[ks];
+        *out = tab.alpha[ks];
+        return IPM_OK;
+      };
+      // (b) reference-exact (IPM_LS_EXACT): every trial point next_x = x + a dx is formed, its
+      //     slacks come from a fresh d - C next_x GEMV when the reference refreshes them, and
+      //     f(next_x) is evaluated directly (P next_x GEMV) -- NewtonSolver.py:165-206 step by step,
+      //     one device->host copy per trial
+      auto exact_step = [&](double* out) -> int {
+        const ipm_problem_desc& dd = pr->d;
+        double f_cur = 0.0, sl_cur = 0.0;
+        bool feas = true;
+        auto eval_at = [&](double a, bool fresh) -> int {
+          lincomb(st, pr->N, 1.0, x, a, pr->dx, pr->xd);
+          ReduceBatch rbt{};
+          int cnt = 0;
+          if (!pr->lp && !pr->ph1 && dd.P) gemv_n(st, pr->n, pr->n, 1.0, dd.P, dd.ldp, pr->xd, 0.0, pr->Px);
+          objective_parts(pr, pr->xd, rbt, cnt);
+          fill(st, pr->scal, SC_COUNT, 0.0);
+          reduce(st, rbt, cnt, pr->scal);
+          if (fresh && pr->S > 0) {
+            compute_slacks(pr, pr->xd, pr->sdv, nullptr, nullptr);
+            // candidate 0 of a pass with alpha0 = 0 is the fresh slack vector itself
+            ls_lin(st, pr->S, pr->Sbar, pr->sdv, pr->ds, 0.0, o->beta, pr->pmask, pr->psum);
+            ls_fold(st, ls_lin_blocks(pr->S), pr->pmask, pr->psum, pr->mask, pr->sums);
+          }
+          Readback r{};
+          const int rc2 = readback(pr, r, false);
+          if (rc2) return rc2;
+          f_cur = f_at(pr, r.sc, 0.0);
+          if (fresh) {
+            feas = pr->S > 0 ? (r.mask & 1ull) != 0 : true;
+            sl_cur = pr->S > 0 ? r.sums[0] : 0.0;
+          }
+          return IPM_OK;
+        };
+        double a = 1.0;
+        int rc2 = eval_at(a, true);
+        if (rc2) return rc2;
+        while (!feas) {                              // domain loop (NewtonSolver.py:172-183)
+          a *= o->beta;
+          if (a < STEP_FLOOR) { *out = a; return IPM_OK; }
+          rc2 = eval_at(a, true);
+          if (rc2) return rc2;
+        }
+        int attempt = 0;                             // Armijo loop (NewtonSolver.py:185-202)
+        while (t * f_cur - sl_cur > fx + o->alpha * a * gc) {
+          ++attempt;
+          const double a_pt = a;                     // next_x = x + a dx BEFORE a *= beta (Q3)
+          if (a < STEP_FLOOR) { *out = a; return IPM_OK; }
+          a *= o->beta;
+          rc2 = eval_at(a_pt, K > 0 && attempt % K == K - 1);
+          if (rc2) return rc2;
+        }
+        *out = a;
+        return IPM_OK;
+      };
+      double step = 0.0;
+      const int lsm = o->linesearch_mode;
+      if (lsm != IPM_LS_EXACT) {
+        rc = table_step(&step);
+        if (rc) return rc;
+      }
+      if (lsm == IPM_LS_EXACT || lsm == IPM_LS_COMPARE) {
+        if (pr->socp) {
+          h->err = "reference-exact line search: LP / QP / phase 1 only";
+          return IPM_NOT_SUPPORTED;
+        }
+        const Readback rb0 = rb;                     // g.x, g.dx, x[n], dx[n] of this step
+        double se = 0.0;
+        rc = exact_step(&se);
+        if (rc) return rc;
+        rb = rb0;
+        if (lsm == IPM_LS_COMPARE) {
+          ++res->ls_compared;
+          if (se != step) ++res->ls_flips;
+        }
+        step = se;
       }
       axpy(st, pr->N, step, pr->dx, x);
       res->last_step = step;

@@ -5,6 +5,7 @@ Host code: this package (Python, mirrors the reference's classes).
 Device code: libipm355.so (hand-written HIP for gfx950, C ABI in include/ipm355.h).
 """
 from ._lib import IPMBackendError, load_library  # noqa: F401
+from .device import set_linesearch_mode  # noqa: F401
 from .lasso import LassoSolver  # noqa: F401
 from .function_manager import (FunctionManagerLP, FunctionManagerPhase1, FunctionManagerQP,  # noqa: F401
                                FunctionManagerSOCP, FunctionManagerSOCPPhase1)

@@ -21,6 +21,7 @@ IPM_HIP_ERROR = 3
 
 KIND_LP, KIND_QP, KIND_SOCP = 0, 1, 2
 SOLVE_CHOLESKY, SOLVE_DIAGONAL, SOLVE_LU = 0, 1, 2
+LS_TABLE, LS_EXACT, LS_COMPARE = 0, 1, 2
 
 P = C.c_void_p
 I32 = C.c_int32
@@ -51,12 +52,13 @@ class ProblemDesc(C.Structure):
 class NewtonOpts(C.Structure):
     _fields_ = [("max_iters", I32), ("update_slacks_every", I32), ("phase1_flag", I32),
                 ("use_psd_condition", I32), ("eps", F64), ("alpha", F64), ("beta", F64),
-                ("phase1_tol", F64), ("trace", C.POINTER(F64)), ("trace_cap", I32), ("reserved", I32)]
+                ("phase1_tol", F64), ("trace", C.POINTER(F64)), ("trace_cap", I32), ("linesearch_mode", I32)]
 
 
 class NewtonResult(C.Structure):
     _fields_ = [("iters", I32), ("success", I32), ("stat_valid", I32), ("use_backup", I32),
-                ("stat", F64), ("last_step", F64), ("backtracks", I64)]
+                ("stat", F64), ("last_step", F64), ("backtracks", I64), ("ls_compared", I64),
+                ("ls_flips", I64)]
 
 
 EXPORTS = {

@@ -30,6 +30,32 @@ def expand_bound(b, n):
     return np.full(n, float(b)) if b.ndim == 0 else b.astype(np.float64, copy=False)
 
 
+
+_LS_MODES = {"table": 0, "exact": 1, "compare": 2}
+_ls_mode = None
+
+
+def set_linesearch_mode(mode):
+    """Feasible-start backtracking (NewtonSolver.py:157-206) for solves started after this call:
+    "table" (default: 64 candidate steps per pass, decisions replayed on the host), "exact"
+    (reference-exact: every trial point formed, fresh slacks by GEMV when the reference refreshes
+    them, f evaluated directly; one device->host copy per trial), "compare" (both; the exact step is
+    taken and disagreements are counted in DeviceProblem.ls_flips / ls_compared).  Default from
+    the environment variable IPM_LINESEARCH."""
+    global _ls_mode
+    if mode not in _LS_MODES:
+        raise ValueError(f"linesearch mode must be one of {sorted(_LS_MODES)}")
+    _ls_mode = mode
+
+
+def linesearch_mode():
+    import os
+    m = _ls_mode or os.environ.get("IPM_LINESEARCH", "table")
+    if m not in _LS_MODES:
+        raise ValueError(f"IPM_LINESEARCH must be one of {sorted(_LS_MODES)}, got {m!r}")
+    return _LS_MODES[m]
+
+
 class ConeData:
     """Stacked second-order-cone data (ipm_problem_desc SOCP fields).
 
@@ -164,6 +190,7 @@ class DeviceProblem:
         o = L.NewtonOpts(int(max_iters), int(update_slacks_every), 1 if phase1_flag else 0,
                          1 if use_psd_condition else 0, float(eps), float(alpha), float(beta),
                          float(phase1_tol))
+        o.linesearch_mode = linesearch_mode()
         cap = int(max_iters)
         buf = (ct.c_double * (2 * max(cap, 1)))()
         o.trace = ct.cast(buf, ct.POINTER(ct.c_double))
@@ -173,6 +200,8 @@ class DeviceProblem:
                                                     ct.byref(r))
         k = min(int(r.iters), cap)
         self.last_trace = [(buf[2 * i], buf[2 * i + 1]) for i in range(k)]
+        self.ls_compared = getattr(self, "ls_compared", 0) + int(r.ls_compared)
+        self.ls_flips = getattr(self, "ls_flips", 0) + int(r.ls_flips)
         return r
 
     def kkt_flops(self):

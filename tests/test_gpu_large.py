@@ -148,6 +148,33 @@ def test_m3_truncated_trajectory(name):
         assert nd_x <= 1.0, nd_x
 
 
+@pytest.mark.parametrize("name", ["m2_qp", "m3_qp_ph1", "m3_qp_feas", "m3_lp"])
+def test_linesearch_flip_rate(name, monkeypatch):
+    """The 64-candidate table line search against the reference-exact one (IPM_LINESEARCH=compare:
+    every Newton step runs both, takes the exact step and counts the steps whose sizes differ) on
+    the M2 and M3 trajectories; the trajectory must still meet the fixture's bars."""
+    import json
+    monkeypatch.setenv("IPM_LINESEARCH", "compare")
+    z = _fixture(name)
+    spec, kw = _instance(z)
+    s = _cls(spec)(check_cvxpy=False, suppress_print=True, **kw)
+    if "k_steps" in z:
+        s.solve(iteration_budget=int(z["k_steps"]))
+    else:
+        s.solve()
+    probs = [s.fm.prob] + ([s.phase1_solver.phase1_fm.prob] if s.phase1_solver is not None else [])
+    cmp_, flips = sum(getattr(p, "ls_compared", 0) for p in probs), sum(getattr(p, "ls_flips", 0) for p in probs)
+    steps, nds = _device_trace(s)
+    same = np.array_equal(steps, z["trace_step"]) if len(steps) == len(z["trace_step"]) else False
+    print(f"[{name}] line-search flips {flips} of {cmp_} Newton steps; step sequence equal to the reference: {same}")
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", f"ls_flips_{name}.json"), "w") as f:
+        json.dump({"case": name, "compared": cmp_, "flips": flips, "steps_equal_reference": bool(same)}, f)
+    assert cmp_ == len(steps)
+    if bool(z["sens_steps_stable"]):
+        assert same
+
+
 def test_m4_shard_on_one_gpu():
     """Config 4 shard: eight of the 64 M4 instances (seeds 1000..1007, n=2048, m=512) solved by the
     sharded driver (ipm355.dist.solve_sharded, world 1 -> every instance on this GPU), x* gathered

@@ -122,6 +122,29 @@ def test_full_solve_matches_reference(name):
               f"iters {list(s.inner_iters)} vs {list(z['inner_iters'])}")
 
 
+EXACT_CASES = sorted(k for k, v in SOLVE_CASES.items() if v != "SOCP" and not k.startswith("lp_eq"))
+
+
+@pytest.mark.parametrize("name", EXACT_CASES)
+def test_full_solve_reference_exact_linesearch(name, monkeypatch):
+    """IPM_LINESEARCH=exact (every trial point formed, fresh slacks by GEMV, f evaluated directly,
+    NewtonSolver.py:165-206 step by step): the same bars as the default table replay."""
+    monkeypatch.setenv("IPM_LINESEARCH", "compare")
+    z, s, v = _run(name)
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    err = rel(s.xstar, z["xstar"])
+    probs = [s.fm.prob] + ([s.phase1_solver.phase1_fm.prob] if s.phase1_solver is not None else [])
+    cmp_, flips = sum(getattr(p, "ls_compared", 0) for p in probs), sum(getattr(p, "ls_flips", 0) for p in probs)
+    print(f"[{name}] exact line search: x* rel {err:.1e}, table/exact step flips {flips} of {cmp_}")
+    assert cmp_ > 0
+    assert err <= xtol
+    if bool(z["sens_iters_stable"]):
+        assert list(s.inner_iters) == list(z["inner_iters"])
+        steps = [t[0] for t in ((s.phase1_solver.phase1_ns.trace if len(z["phase1_inner_iters"]) else [])
+                                + s.ns.trace)]
+        np.testing.assert_array_equal(np.array(steps), z["trace_step"])
+
+
 def test_group_lasso_fstar_known_answer():
     """demo.ipynb cell 31: exercises the Cholesky-failure fallback in SOCP phase 1."""
     z, s, v = _run("socp_group_lasso")
