@@ -100,16 +100,23 @@ def launch_ranks(n):
                           extra_env={"IPM_BENCH_BACKEND": backend})
 
 
-def make_instance(n, m, seed, dev):
+def make_instance(n, m, seed, dev, problem="qp"):
     """M3-QP instance (grid values); P = Pp^T Pp + I with the Gram product on the device (setup only,
-    exact on the grid, not timed)."""
+    exact on the grid, not timed).  problem="lp": the M3-LP generator (testSolver.py:104-148);
+    "socp": M5 (n variables, m cones of 16 rows, strictly feasible x0 -> barrier phase only)."""
     import torch
     from ipm355 import problems
 
     def gram(Pp):
         t = torch.as_tensor(Pp, device=dev)
         return (t.T @ t).cpu().numpy()
-    inst = problems.qp_ineq_box(n, m, seed=seed, grid=True, with_xf=True, gram=gram)
+    if problem == "socp":
+        inst = problems.socp_cones(n=n, K=m, mi=16, seed=seed)
+        return inst, inst.pop("x0")
+    if problem == "lp":
+        inst = problems.lp_ineq_box(n, m, seed=seed, grid=True, with_xf=True)
+    else:
+        inst = problems.qp_ineq_box(n, m, seed=seed, grid=True, with_xf=True, gram=gram)
     xf = inst.pop("xf")
     return inst, xf
 
@@ -182,6 +189,8 @@ def main():
                     help="which phase(s) the timed steps run in (default: half each)")
     ap.add_argument("--concurrent", action="store_true",
                     help="solve the instances concurrently: one HIP stream + host thread each")
+    ap.add_argument("--problem", choices=["qp", "lp", "socp"], default="qp",
+                    help="qp: the headline M3-QP (default); lp: M3-LP (config 3); socp: M5, --m = cones (config 5)")
     ap.add_argument("--instances", type=int, default=1,
                     help="independent instances per GPU (config 4: --n 2048 --m 512 --instances 8); each runs "
                          "`steps` Newton iterations")
@@ -191,8 +200,8 @@ def main():
     if args.concurrent:
         # each instance = its stream + its Cholesky panel stream; HIP maps streams onto
         # GPU_MAX_HW_QUEUES hardware queues (4 by default) -- streams sharing a queue serialise.
-        # Must be set before the HIP runtime starts.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+        # Must be set before the HIP runtime starts (the box presets 4: override it, <= 32 allowed).
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("IPM_HW_QUEUES", "16")
 
     import torch
     import torch.distributed as dist
@@ -219,25 +228,28 @@ def main():
     from ipm355 import dist as D
     from ipm355 import problems
 
-    kwargs = dict(problems.QP_KWARGS)
+    kwargs = dict({"qp": problems.QP_KWARGS, "lp": problems.LP_KWARGS, "socp": problems.SOCP_KWARGS}[args.problem])
+    Cls = {"qp": ipm355.QPSolver, "lp": ipm355.LPSolver, "socp": ipm355.SOCPSolver}[args.problem]
     if args.instances == 1:
         seeds = [rank]                         # headline: one n=8192 instance per GPU, seed = rank
     else:                                      # config 4: instances r::world of world*I, seeds 1000 + index
         seeds = [1000 + i for i in D.shard(args.instances * world, rank, world)]
-    insts = [make_instance(args.n, args.m, seed=sd, dev=dev) for sd in seeds]
+    insts = [make_instance(args.n, args.m, seed=sd, dev=dev, problem=args.problem) for sd in seeds]
 
     def new_solver(k, feasible):
         inst, xf = insts[k]
         kw = dict(inst, **kwargs)
         if feasible:
             kw["x0"] = xf.copy()               # strictly feasible -> phase 1 skipped (Q11)
-        return ipm355.QPSolver(check_cvxpy=False, suppress_print=True, device=dev_index, **kw)
+        return Cls(check_cvxpy=False, suppress_print=True, device=dev_index, **kw)
 
     streams = [torch.cuda.Stream(device=dev) for _ in insts] if args.concurrent else [None] * len(insts)
 
     def on(stream):
         return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
+    if args.problem == "socp":
+        args.phase = "barrier"               # M5 starts strictly feasible (phase 1 skipped, Q11)
     k1 = {"both": (args.steps + 1) // 2, "phase1": args.steps, "barrier": 0}[args.phase]
     segs = [("phase1", k1), ("barrier", args.steps - k1)]
     w1 = (args.warmup + 1) // 2
@@ -245,7 +257,7 @@ def main():
         if budget > 0:
             for k in range(len(insts) if args.concurrent else 1):
                 with on(streams[k]):
-                    new_solver(k, feasible).solve(iteration_budget=budget)
+                    new_solver(k, feasible or args.problem == "socp").solve(iteration_budget=budget)
     with on(streams[0]):
         h = L.Handle.get(dev_index)
     import ctypes
@@ -368,7 +380,11 @@ def main():
             "newton_iters": total_iters,
             "lib_sha256": lib_digest(),
         }
-        if not args.no_cpu and world == 1:
+        if args.problem != "qp":
+            rec["metric"] = f"Newton iters/sec, dense {args.problem.upper()} (config {'3' if args.problem == 'lp' else '5'})"
+            rec["config"]["workload"] = rec["config"]["workload"].replace("QPSolver", Cls.__name__).replace(
+                "dense QP", "dense " + args.problem.upper())
+        if not args.no_cpu and world == 1 and args.problem == "qp":
             rec["cpu_baseline"] = cpu_baseline(insts[0][0], kwargs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
