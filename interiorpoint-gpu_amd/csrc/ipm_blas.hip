@@ -15,6 +15,9 @@
 #include "ipm_mfma.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <queue>
 #include <cmath>
 #include <vector>
 #include <cstdlib>
@@ -925,6 +928,11 @@ struct BlockArgs {
   // has 1-2 rows past a multiple of 128)
   int64_t rag_r0 = 0;
   int rag_n = 0, nrag = 0;
+  // trailing tiles split in two K halves (the planner's pick for the launch's last round):
+  // S tickets [0, s_full) are whole tiles, then two per split tile (tile s_full + p)
+  int64_t s_full = 0;
+  double* sscr = nullptr;       // split p's upper-half partial tile at sscr + p * 128 * 128
+  unsigned* sflag = nullptr;    // split p done: sflag[p]
 };
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
@@ -1316,7 +1324,14 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       __syncthreads();
       const int v = sflag;
       __syncthreads();
-      if (v) mfma_tile<128, false, VEC, 2, false>(b.s, v - 1, sm.g128);
+      if (v) {
+        // S ticket -> whole tile, or one K-half of a split tile (pieces: upper half, then lower)
+        const int64_t st = v - 1, u = st - b.s_full;
+        const int sp = u < 0 ? 0 : ((u & 1) ? 2 : 1);
+        const int64_t p = u < 0 ? 0 : (u >> 1);
+        mfma_tile<128, false, VEC, 2, false>(b.s, u < 0 ? st : b.s_full + p, sm.g128, sp, b.sscr + p * (128 * 128),
+                                             b.sflag + p);
+      }
     }
   }
 }
@@ -1337,6 +1352,46 @@ static void zero2(hipStream_t st, void* a, int64_t na, void* b, int64_t nb) {
                        reinterpret_cast<unsigned*>(b), nb);
 }
 
+// ---- split planner: how many of a launch's trailing tiles to cut into two K halves.  The
+// launch is list-scheduled on the host (2 workgroup slots per CU, items in ticket order, durations
+// in units of one 128 x 128 x 256 trailing tile, ~100 us; role durations from the IPM_ROLE_TRACE
+// timelines in DESIGN.md): whole tiles 1.0, half tiles 0.55, row chunks 0.5, look-ahead tiles 0.8,
+// P(a) / P(b) diagonal roles 0.6 / 1.25.  The q with the smallest makespan wins (0 when the launch
+// is chain-bound).  Splitting the LAST q tiles turns a last round that would hold a few whole
+// tiles into one of half tiles running on twice as many slots.
+static int num_cus();
+static double split_makespan(int slots, const std::vector<std::pair<int64_t, double>>& items) {
+  std::priority_queue<double, std::vector<double>, std::greater<double>> q;
+  for (int i = 0; i < slots; ++i) q.push(0.0);
+  double mk = 0.0;
+  for (const auto& it : items)
+    for (int64_t k = 0; k < it.first; ++k) {
+      const double t = q.top() + it.second;
+      q.pop();
+      q.push(t);
+      mk = std::max(mk, t);
+    }
+  return mk;
+}
+static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t ns, int64_t nrows,
+                          int64_t cap) {
+  if (ns < 64) return 0;
+  const int slots = 2 * num_cus();
+  auto mk = [&](int64_t q) {
+    std::vector<std::pair<int64_t, double>> it = {{nla, 0.8}, {1, 0.6}, {nchd, 0.66}, {nnf, 0.8}, {pb ? 1 : 0, 1.25},
+                                                  {nrag, 0.1}, {ns - q, 1.0}, {2 * q, 0.55}, {nrows, 0.5}};
+    return split_makespan(slots, it);
+  };
+  const double m0 = mk(0);
+  double best = m0;
+  int64_t bq = 0;
+  for (int64_t q = 8; q <= std::min(ns, cap); q += 8) {
+    const double m = mk(q);
+    if (m < best - 0.02) { best = m; bq = q; }
+  }
+  return bq;
+}
+
 void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
                        const DeferSyrk* ds) {
   const bool defer = ds && ds->active();
@@ -1353,6 +1408,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   // IPM_RAG=0: ragged trailing rows as a row of 128-tiles (read per call: tests compare both)
   const char* erag = getenv("IPM_RAG");
   const bool rag_on = !(erag && erag[0] == '0');
+  // IPM_SPLIT=0: no K-split trailing tiles (read per call: tests compare both)
+  const char* esp = getenv("IPM_SPLIT");
+  const bool split_on = !(esp && esp[0] == '0');
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     BlockArgs b;
     b.n = n;
@@ -1457,6 +1515,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         g.tiles_i = cdiv(ms, 128);
         g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
         b.ns = g.nblk;
+        b.s_full = b.ns;
       }
     }
 #ifdef IPM_ROLE_TRACE
@@ -1470,6 +1529,30 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     {
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
+    }
+    if (b.ns > 0 && !defer && split_on) {
+      // the planner's split count (cached per size and block: it depends on nothing else)
+      static std::mutex mu;
+      static std::map<std::pair<int64_t, int64_t>, std::vector<int64_t>> cache;
+      const int nchd_h = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
+      int64_t q = 0;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& v = cache[{n, ncols}];
+        if ((int64_t)v.size() < nblocks) v.assign(nblocks, -1);
+        if (v[bk] < 0) {
+          v[bk] = plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.ns, (b.nra - nchd_h) + b.nrb,
+                             potrf_split_cap(n));
+          static const bool dbg = getenv("IPM_SPLIT_DEBUG") != nullptr;
+          if (dbg) fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld\n", (long)n, (long)bk,
+                           (long)b.ns, (long)v[bk]);
+        }
+        q = v[bk];
+      }
+      b.s_full = b.ns - q;
+      b.ns = b.s_full + 2 * q;
+      b.sscr = ws + potrf_split_scratch_off(n);
+      b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
     }
     if (defer) {
       // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
@@ -1527,7 +1610,7 @@ int defer_plan(int64_t ns, int64_t m, int KS, int nblocks, int* d, unsigned long
   const int64_t N = (int64_t)nblocks * CH_NB;           // rows of the factored matrix (approx.)
   const double fill = env_d("IPM_DEFER_FILL", 0.6), chain_us = env_d("IPM_DEFER_CHAIN_US", 115);
   const double ucost = env_d("IPM_DEFER_UNIT_US", 25) * 256.0 / KS;   // one 64-tile slice task
-  const int slots = 2 * num_cus_host();
+  const int slots = 2 * num_cus();
   std::vector<double> cap(nblocks, 0.0);
   std::vector<int> jobs(nblocks, 0);
   for (int L = 1; L < nblocks; ++L) {

@@ -64,10 +64,19 @@ void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A
 // ws: device workspace of potrf_ws_doubles(n) doubles: two panels' inverted diagonal blocks and
 // published L11 blocks, then the control words (per launch: a header, one word per 64-row block
 // for the look-ahead tiles and one per 64-row chunk of the first panel)
-__host__ __device__ inline int64_t block_ctl_words(int64_t n) { return 56 + 2 * ((n + 63) / 64) + 8; }
-inline int64_t potrf_ws_doubles(int64_t n) {
-  return 2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8;
+// trailing tiles a launch may split in two K halves (its last round): flags in the control
+// words, one 128 x 128 partial tile each in the workspace
+__host__ __device__ inline int64_t potrf_split_cap(int64_t n) {
+  const int64_t t = (n + 127) / 128, tri = t * (t + 1) / 2;
+  return tri < 512 ? tri : 512;
 }
+__host__ __device__ inline int64_t block_ctl_words(int64_t n) {
+  return 56 + 2 * ((n + 63) / 64) + 8 + potrf_split_cap(n);
+}
+inline int64_t potrf_split_scratch_off(int64_t n) {
+  return ((2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8) + 31) & ~int64_t(31);
+}
+inline int64_t potrf_ws_doubles(int64_t n) { return potrf_split_scratch_off(n) + potrf_split_cap(n) * 128 * 128; }
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
 
 // KKT SYRK slices deferred into the Cholesky (the Newton step's  H = tP + C^T diag(w) C + diag):

@@ -93,8 +93,14 @@ struct alignas(16) MfSmem {
 // SC1OUT: the tile is stored with sc1 stores (read by other workgroups of the same launch).
 // FOLD: a.C2 is folded into the start value (the Cholesky look-ahead tiles taking the deferred
 // KKT slices); a separate instantiation keeps the other tiles' register budget.
+// split (Cholesky trailing tiles of a launch's last round, sub tiles only): the K range is cut in
+// two halves computed by two workgroups at once.  SPLIT 1 (the LOWER ticket): k in [K/2, K), the
+// accumulators start at 0, the tile -X^T Y goes to the scratch tile `part` (sc1, 128 x 128
+// column-major), then *pflag = 1.  SPLIT 2: k in [0, K/2) from the C tile as usual; before its
+// stores it waits for *pflag and adds `part`.  Only ever waits on a lower ticket.
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false>
-__device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm) {
+__device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
+                                          double* part = nullptr, unsigned* pflag = nullptr) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
   auto& sX = sm.sX;
@@ -124,12 +130,15 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wi = wv & 1, wj = wv >> 1;
   const int sr = tid / TPR, sc = (tid % TPR) * PT;
-  const double* xp = a.X + sr * a.ldx + I0 + sc;
-  const double* yp = a.Y + sr * a.ldy + J0 + sc;
+  const int64_t kbeg = SPLIT == 1 ? a.K / 2 : 0;
+  const double* xp = a.X + (sr + kbeg) * a.ldx + I0 + sc;
+  const double* yp = a.Y + (sr + kbeg) * a.ldy + J0 + sc;
   const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
   // K extent of this tile (the KKT SYRK with deferred slices: columns ahead take fewer k rows)
   int kt32 = (int)a.K;
   if (a.kend256) kt32 = __builtin_amdgcn_readfirstlane(std::min(kt32, a.kend256[J0 >> 8]));
+  if (SPLIT == 1) kt32 = kt32 - kt32 / 2;
+  if (SPLIT == 2) kt32 = kt32 / 2;
   const int64_t Kt = kt32;
   const int64_t nslab = (Kt + BK - 1) / BK;
   // C -= X^T Y (Cholesky updates): the accumulators start FROM the C tile (its loads overlap the
@@ -185,7 +194,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   for (int u = 0; u < TWJ; ++u)
 #pragma unroll
     for (int v = 0; v < TWI; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
-  if (cinit) {
+  if (cinit && SPLIT != 1) {
 #pragma unroll
     for (int tj = 0; tj < TWJ; ++tj)
 #pragma unroll
@@ -231,6 +240,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   }
   // ---- epilogue: lane holds D[j = fk + 4r][i = fr] of each 16 x 16 tile (f64 MFMA map,
   //      cdna_hip_programming.md §3) -> 16 consecutive lanes store 16 consecutive i
+  if (SPLIT == 2) {
+    if (tid == 0)
+      while (__hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+  }
 #pragma unroll
   for (int tj = 0; tj < TWJ; ++tj)
 #pragma unroll
@@ -239,11 +253,15 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
-        if (i < a.ni && j < a.nj && (!a.tri || i >= j)) {
+        if (SPLIT == 1) {
+          st_sc1(&part[(j - J0) * BM + (i - I0)], acc[tj][ti][r]);
+        } else if (i < a.ni && j < a.nj && (!a.tri || i >= j)) {
           double* cp = a.C + j * a.ldc + i;
           if (cinit) {
-            if (SC1OUT) st_sc1(cp, acc[tj][ti][r]);
-            else *cp = acc[tj][ti][r];
+            double v = acc[tj][ti][r];
+            if (SPLIT == 2) v += ld_sc1(&part[(j - J0) * BM + (i - I0)]);
+            if (SC1OUT) st_sc1(cp, v);
+            else *cp = v;
           } else {
             double v = a.alpha * acc[tj][ti][r];
             if (a.beta != 0.0) v += a.beta * (*cp);
@@ -254,6 +272,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
         }
       }
     }
+  if (SPLIT == 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(pflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
