@@ -193,6 +193,14 @@ int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double* H, int64_
 /* solve L L^T X = B in place; L lower column-major (ldl); B row-major n x nrhs (ldb) */
 int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
               int64_t ldb);
+/* LU with partial pivoting, in place (column-major, lda): the np.linalg.solve / Cholesky-fallback
+   factorisation (NewtonSolver.py:230-247, 334-341; NewtonSolverInfeasibleStart.py:513-538).  Blocked:
+   64-column panels, MFMA trailing update.  piv [dev] n: row swapped with k, or -1-k for an exactly
+   zero pivot column (skipped; ipm_getrs gives that component 0) */
+int ipm_getrf(ipm_handle* h, int64_t n, double* A, int64_t lda, int64_t* piv, int* info);
+/* solve with the ipm_getrf factors; B row-major n x nrhs (ldb), in place */
+int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
+              double* B, int64_t ldb);
 /* HIP-event timing of the KKT assembly and of the Cholesky factorisation inside
    ipm_newton_solve (enable/reset with ipm_set_timing; adds no synchronisation):
    averages (ms) over the Newton iterations since the reset, and their count */

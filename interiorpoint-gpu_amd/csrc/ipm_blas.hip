@@ -2336,8 +2336,18 @@ void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64
 // piv = -1 - row and skipped; getrs then sets that unknown to 0 (the minimum-norm choice
 // when the null space is that coordinate -- see DESIGN.md, fallback semantics).
 // =====================================================================================
+// ---- LU with partial pivoting (np.linalg.solve; the Cholesky fallback, Q9), column-major.
+// Blocked right-looking: panels of LU_NB columns are factored column by column (pivot search,
+// swap and scale in one workgroup; the rank-1 update restricted to the panel), then the panel's
+// row swaps go to the other columns (k_laswp), U12 = L11^-1 A12 (k_lu_trsm) and the trailing
+// matrix takes A22 -= L21 U12 as ONE fp64-MFMA GEMM (the trailing update of the unblocked form
+// re-streamed the whole matrix once per column).  Pivot choice = LAPACK's (first index of the
+// largest |a|).  An exactly zero pivot column is skipped (piv = -1 - k, its L column zeroed so the
+// blocked updates see no contribution), like the unblocked form: getrs then gives that component 0.
+constexpr int LU_NB = 64;
+
 __global__ __launch_bounds__(1024) void k_lu_pivot(int64_t n, int64_t k, double* __restrict__ A,
-                                                   int64_t lda, int64_t* __restrict__ piv) {
+                                                   int64_t lda, int64_t* __restrict__ piv, int64_t j0, int64_t j1) {
   __shared__ double sv[1024];
   __shared__ int64_t si[1024];
   const int tid = threadIdx.x;
@@ -2361,11 +2371,12 @@ __global__ __launch_bounds__(1024) void k_lu_pivot(int64_t n, int64_t k, double*
   const double pv = sv[0];
   if (!(pv > 0.0)) {
     if (tid == 0) piv[k] = -1 - k;
+    for (int64_t i = k + 1 + tid; i < n; i += 1024) A[k * lda + i] = 0.0;   // no L contribution
     return;
   }
-  // swap rows k and p across all columns
+  // swap rows k and p in columns [j0, j1) (the panel; k_laswp does the others)
   if (p != k) {
-    for (int64_t j = tid; j < n; j += 1024) {
+    for (int64_t j = j0 + tid; j < j1; j += 1024) {
       double t = A[j * lda + k];
       A[j * lda + k] = A[j * lda + p];
       A[j * lda + p] = t;
@@ -2377,24 +2388,88 @@ __global__ __launch_bounds__(1024) void k_lu_pivot(int64_t n, int64_t k, double*
   for (int64_t i = k + 1 + tid; i < n; i += 1024) A[k * lda + i] /= d;
 }
 
+// rank-1 update of the panel columns (k, j1)
 __global__ __launch_bounds__(256) void k_lu_update(int64_t n, int64_t k, double* __restrict__ A,
-                                                   int64_t lda, const int64_t* __restrict__ piv) {
+                                                   int64_t lda, const int64_t* __restrict__ piv, int64_t j1) {
   if (piv[k] < 0) return;
   const int64_t j = k + 1 + blockIdx.y;
   const int64_t i = k + 1 + (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= n || i >= n) return;
+  if (j >= j1 || i >= n) return;
   const double ukj = A[j * lda + k];
   if (ukj != 0.0) A[j * lda + i] -= A[k * lda + i] * ukj;
 }
 
-void getrf(hipStream_t st, int64_t n, double* A, int64_t lda, int64_t* piv, int* info) {
-  hipMemsetAsync(info, 0, sizeof(int), st);
-  for (int64_t k = 0; k < n; ++k) {
-    hipLaunchKernelGGL(k_lu_pivot, dim3(1), dim3(1024), 0, st, n, k, A, lda, piv);
-    if (k + 1 < n) {
-      dim3 g(cdiv(n - k - 1, 256), n - k - 1);
-      hipLaunchKernelGGL(k_lu_update, g, dim3(256), 0, st, n, k, A, lda, piv);
+// the panel's swaps (rows k0 .. k0+kb-1, in order) applied to columns outside [k0, k0+kb)
+__global__ __launch_bounds__(256) void k_laswp(int64_t n, int64_t k0, int64_t kb, double* __restrict__ A,
+                                               int64_t lda, const int64_t* __restrict__ piv) {
+  int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n - kb) return;
+  if (j >= k0) j += kb;
+  double* col = A + j * lda;
+  for (int64_t k = k0; k < k0 + kb; ++k) {
+    const int64_t p = piv[k];
+    if (p >= 0 && p != k) {
+      const double t = col[k];
+      col[k] = col[p];
+      col[p] = t;
     }
+  }
+}
+
+// U12 = L11^-1 A12 (unit lower L11 = rows/cols k0..k0+kb of A) for columns j >= k0 + kb, written in
+// place and also to T (kb x m, k-major: T[q * ldt + jj]) -- the GEMM operand of the trailing update
+__global__ __launch_bounds__(256) void k_lu_trsm(int64_t n, int64_t k0, int64_t kb, double* __restrict__ A,
+                                                 int64_t lda, double* __restrict__ T, int64_t ldt) {
+  __shared__ double sL[LU_NB * LU_NB];
+  for (int64_t e = threadIdx.x; e < kb * kb; e += 256) {
+    const int64_t c = e / kb, r = e - c * kb;
+    sL[c * LU_NB + r] = A[(k0 + c) * lda + k0 + r];
+  }
+  __syncthreads();
+  const int64_t jj = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t j = k0 + kb + jj;
+  if (j >= n) return;
+  double* col = A + j * lda + k0;
+  double x[LU_NB];
+#pragma unroll
+  for (int q = 0; q < LU_NB; ++q) {
+    if (q < kb) {
+      double v = col[q];
+      for (int r = 0; r < q; ++r) v = fma(-sL[r * LU_NB + q], x[r], v);
+      x[q] = v;
+      col[q] = v;
+      T[q * ldt + jj] = v;
+    }
+  }
+}
+
+void getrf(hipStream_t st, int64_t n, double* A, int64_t lda, int64_t* piv, int* info, double* ws) {
+  hipMemsetAsync(info, 0, sizeof(int), st);
+  for (int64_t k0 = 0; k0 < n; k0 += LU_NB) {
+    const int64_t kb = std::min<int64_t>(LU_NB, n - k0), j1 = k0 + kb;
+    for (int64_t k = k0; k < j1; ++k) {
+      hipLaunchKernelGGL(k_lu_pivot, dim3(1), dim3(1024), 0, st, n, k, A, lda, piv, k0, j1);
+      if (k + 1 < j1 && k + 1 < n) {
+        dim3 g((unsigned)cdiv(n - k - 1, 256), (unsigned)(j1 - k - 1));
+        hipLaunchKernelGGL(k_lu_update, g, dim3(256), 0, st, n, k, A, lda, piv, j1);
+      }
+    }
+    if (n - kb > 0) hipLaunchKernelGGL(k_laswp, dim3((unsigned)cdiv(n - kb, 256)), dim3(256), 0, st, n, k0, kb, A, lda, piv);
+    const int64_t m = n - j1;
+    if (m <= 0) continue;
+    hipLaunchKernelGGL(k_lu_trsm, dim3((unsigned)cdiv(m, 256)), dim3(256), 0, st, n, k0, kb, A, lda, ws, m);
+    // A22 -= L21 U12: C(i, j) -= sum_q X[q][i] Y[q][j], X = L21 (column q of A, k-major), Y = T
+    GemmArgs g;
+    g.ni = g.nj = m;
+    g.K = kb;
+    g.X = A + k0 * lda + j1;
+    g.ldx = lda;
+    g.Y = ws;
+    g.ldy = m;
+    g.C = A + j1 * lda + j1;
+    g.ldc = lda;
+    g.sub = 1;
+    mfma_gemm_launch(st, g);
   }
 }
 

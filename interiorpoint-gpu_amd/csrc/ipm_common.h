@@ -137,7 +137,9 @@ void trsm_lower_bwd(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int
                     int64_t ldb, double* Y);
 // LU with partial pivoting (row-major in/out copy in column-major work), solve; used as the
 // Cholesky fallback (NewtonSolver.py:334-341, NewtonSolverInfeasibleStart.py:513-538)
-void getrf(hipStream_t s, int64_t n, double* A, int64_t lda, int64_t* piv, int* info_dev);
+// ws: LU_NB * n doubles (the U12 panel operand of the trailing GEMM)
+void getrf(hipStream_t s, int64_t n, double* A, int64_t lda, int64_t* piv, int* info_dev, double* ws);
+inline int64_t getrf_ws_doubles(int64_t n) { return 64 * (n + 1); }
 void getrs(hipStream_t s, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
            double* B, int64_t ldb);
 

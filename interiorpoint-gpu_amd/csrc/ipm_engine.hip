@@ -549,6 +549,26 @@ extern "C" int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L
   return IPM_OK;
 }
 
+extern "C" int ipm_getrf(ipm_handle* h, int64_t n, double* A, int64_t lda, int64_t* piv, int* info) {
+  if (!h || n < 0 || lda < n || !piv) return IPM_INVALID_ARG;
+  if (n == 0) return IPM_OK;
+  double* lw = scratch(h, (size_t)getrf_ws_doubles(n) * sizeof(double));
+  if (!lw) { h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  getrf(h->stream, n, A, lda, piv, h->dinfo, lw);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (info) *info = 0;
+  return IPM_OK;
+}
+
+extern "C" int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
+                         double* B, int64_t ldb) {
+  if (!h || n < 0 || nrhs < 0 || lda < n || ldb < nrhs) return IPM_INVALID_ARG;
+  if (n > 0 && nrhs > 0) getrs(h->stream, n, nrhs, LU, lda, piv, B, ldb);
+  HIPCHK(h, hipGetLastError());
+  return IPM_OK;
+}
+
 extern "C" int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count) {
   // averages over the Newton iterations since ipm_set_timing(h, 1)
   if (!h) return IPM_INVALID_ARG;
@@ -932,7 +952,9 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
     if (rc) return rc;
-    getrf(st, pr->N, pr->H, pr->ldh, pr->piv, pr->info);
+    double* lw = scratch(pr->h, (size_t)getrf_ws_doubles(pr->N) * sizeof(double));
+    if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+    getrf(st, pr->N, pr->H, pr->ldh, pr->piv, pr->info, lw);
     getrs(st, pr->N, 1, pr->H, pr->ldh, pr->piv, pr->dx, 1);
     hipMemsetAsync(pr->info, 0, sizeof(int), st);
   }
@@ -997,7 +1019,9 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   // LU fallback: four np.linalg.solve (NewtonSolverInfeasibleStart.py:513-538)
   int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
   if (rc) return rc;
-  getrf(st, n, pr->H, pr->ldh, pr->piv, pr->info);
+  double* lw = scratch(pr->h, (size_t)std::max(getrf_ws_doubles(n), n * pr->ldh) * sizeof(double));
+  if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  getrf(st, n, pr->H, pr->ldh, pr->piv, pr->info, lw);
   copy(st, pr->Ybuf, d.AT, n * p);
   getrs(st, n, p, pr->H, pr->ldh, pr->piv, pr->Ybuf, p);
   copy(st, pr->tmpn, pr->g, n);
@@ -1006,7 +1030,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
   rc = expand_full_inplace(pr, pr->Sbuf, p, lds);
   if (rc) return rc;
-  getrf(st, p, pr->Sbuf, lds, pr->pivp, pr->info + 1);
+  getrf(st, p, pr->Sbuf, lds, pr->pivp, pr->info + 1, lw);
   gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
   lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
   getrs(st, p, 1, pr->Sbuf, lds, pr->pivp, pr->wv, 1);

@@ -84,6 +84,8 @@ EXPORTS = {
     "ipm_potrf": (C.c_int, [P, I64, P, I64, C.POINTER(C.c_int)]),
     "ipm_potrf_partial": (C.c_int, [P, I64, I64, P, I64, C.POINTER(C.c_int)]),
     "ipm_potrs": (C.c_int, [P, I64, I64, P, I64, P, I64]),
+    "ipm_getrf": (C.c_int, [P, I64, P, I64, P, C.POINTER(C.c_int)]),
+    "ipm_getrs": (C.c_int, [P, I64, I64, P, I64, P, P, I64]),
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),

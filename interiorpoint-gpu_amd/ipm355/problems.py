@@ -156,6 +156,45 @@ def lasso_instance(name):
     return A, b, reg, dict(base, max_iters=1000 if name == "lasso_testsolver" else 400)
 
 
+LP_NPY_ORDER = ("c", "A", "b", "C", "d", "upper_bound", "lower_bound")
+
+
+def save_lp_npy(path, c, A, b, C, d, upper_bound, lower_bound):
+    """The reference's sparse-LP file format (testSolver.py:278-300): seven arrays written one
+    after another into ONE .npy file -- c, A, b, C, d, upper bound, lower bound (dense arrays; the
+    MIPLIB instances aflow40b / 30n20b8 ship in it)."""
+    with open(path, "wb") as f:
+        for a in (c, A, b, C, d, upper_bound, lower_bound):
+            np.save(f, np.asarray(a, dtype=np.float64), allow_pickle=False)
+
+
+def load_lp_npy(path):
+    """Read a file in that format -> LPSolver kwargs (c, A, b, C, d, upper_bound, lower_bound)."""
+    with open(path, "rb") as f:
+        vals = [np.load(f, allow_pickle=False) for _ in LP_NPY_ORDER]
+    return dict(zip(LP_NPY_ORDER, vals))
+
+
+def lp_miplib_like(n=600, p=120, m=240, density=0.03, seed=0):
+    """A MIPLIB-style LP relaxation in the format above (the reference's blobs are absent here):
+    sparse 0/1/integer-coefficient equality rows A x = b and inequality rows C x <= d, box bounds
+    per variable, feasible by construction (x_f strictly inside the bounds, d = C x_f + slack)."""
+    rng = np.random.default_rng(seed)
+
+    def sparse(rows):
+        M = (rng.random((rows, n)) < density) * rng.integers(1, 6, (rows, n)).astype(float)
+        for i in range(rows):                       # at least two nonzeros per row
+            M[i, rng.choice(n, 2, replace=False)] = rng.integers(1, 6, 2)
+        return M
+    lb = np.zeros(n)
+    ub = rng.integers(1, 10, n).astype(float)
+    xf = lb + (ub - lb) * rng.uniform(0.2, 0.8, n)
+    A = sparse(p)
+    C = sparse(m) * rng.choice([-1.0, 1.0], (m, 1))
+    return dict(c=rng.integers(-20, 20, n).astype(float), A=A, b=A @ xf, C=C, d=C @ xf + rng.uniform(0.5, 2.0, m),
+                upper_bound=ub, lower_bound=lb)
+
+
 def instance_seeds(total, rank, world):
     """M4 partitioning (SURVEY.md §8(e)): rank r takes instances r::world."""
     return list(range(rank, total, world))

@@ -13,6 +13,8 @@ SOLVE_CASES = {
     # round 2: feasible NewtonSolverDiagonal (bounds only) and stable diagonal infeasible-start runs
     "lp_box_diag": "LP", "lp_box_diag_vec": "LP",
     "lp_eq_box_tk1": "LP", "lp_eq_box_tk2": "LP", "lp_eq_box_tk1_us5": "LP",
+    # LPs in the reference's sequential .npy format, get_dual_variables=True
+    "lp_npy_miplib": "LP", "lp_ineq_box_duals": "LP", "lp_eq_box_tk1_duals": "LP",
 }
 
 # linear_solve_method np_solve / np_lstsq / direct, pinned by the reference (make_golden.py extra)
@@ -22,7 +24,7 @@ METHOD_CASES = {f"meth_{case}_{meth}": kind
 
 # kwargs that are stored as scalars in the fixture but are not array inputs
 _SCALAR_KW = {"t0", "mu", "epsilon", "alpha", "beta", "max_inner_iters", "max_outer_iters",
-              "update_slacks_every", "lower_bound", "upper_bound", "linear_solve_method"}
+              "update_slacks_every", "lower_bound", "upper_bound", "linear_solve_method", "get_dual_variables"}
 
 
 def load(name):

@@ -169,3 +169,30 @@ def test_potrf_split_trailing_tiles(n, ncols, monkeypatch):
     assert d < 1e-12
     L11 = torch.linalg.cholesky(A[:ncols, :ncols])
     assert ((out["1"][:ncols] - L11).abs().max() / L11.abs().max()).item() < 1e-10
+
+
+@pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 1030, 2100])
+def test_getrf_getrs_match_numpy(n):
+    """Blocked LU with partial pivoting (64-column panels, MFMA trailing update) vs np.linalg.solve;
+    the pivots are LAPACK's (first index of the largest |a|) -- identical to scipy's getrf."""
+    import ctypes
+    import scipy.linalg
+    import torch
+    from gpu_util import handle
+    from ipm355 import _lib as L
+    h = handle()
+    rng = np.random.default_rng(n)
+    A = rng.normal(size=(n, n))
+    Ad = torch.as_tensor(A.T.copy(), device="cuda")        # column-major
+    piv = torch.empty(n, dtype=torch.int64, device="cuda")
+    info = ctypes.c_int(0)
+    assert h.lib.ipm_getrf(h.ptr, n, L.dptr(Ad), n, L.dptr(piv), ctypes.byref(info)) == 0
+    lu_ref, piv_ref = scipy.linalg.lu_factor(A)
+    np.testing.assert_array_equal(piv.cpu().numpy(), piv_ref)
+    LU = Ad.cpu().numpy().T
+    np.testing.assert_allclose(LU, lu_ref, rtol=1e-9, atol=1e-9 * np.abs(lu_ref).max())
+    b = rng.normal(size=(n, 2))
+    Bd = torch.as_tensor(b.copy(), device="cuda")
+    assert h.lib.ipm_getrs(h.ptr, n, 2, L.dptr(Ad), n, L.dptr(piv), L.dptr(Bd), 2) == 0
+    ref = np.linalg.solve(A, b)
+    np.testing.assert_allclose(Bd.cpu().numpy(), ref, rtol=1e-8, atol=1e-10 * np.abs(ref).max())

@@ -104,6 +104,13 @@ def test_full_solve_matches_reference(name):
     s = oracle_solver({**SOLVE_CASES, **METHOD_CASES}[name], kw)
     val = s.solve()
     steps = [tr["step"] for tr in (s.phase1.ns.trace if s.phase1_iters else [])] + [tr["step"] for tr in s.ns.trace]
+    if not bool(z["sens_iters_stable"]) and list(s.inner_iters) != list(z["inner_iters"]):
+        # chaotic in the reference itself (a 1e-15 perturbation or a reordering of the variables
+        # changes its iteration counts): the BLAS thread count here is enough to do the same, so
+        # only the reference's own envelope applies
+        assert rel(s.xstar, z["xstar"]) <= max(1e-9, 4 * float(z["sens_xstar_rel"]))
+        assert rel(val, z["value"]) <= max(1e-9, 4 * float(z["sens_value_rel"]))
+        return
     assert list(s.inner_iters) == list(z["inner_iters"])
     assert list(s.phase1_iters) == list(z["phase1_inner_iters"])
     assert len(steps) == len(z["trace_step"])
