@@ -227,7 +227,7 @@ typedef struct ipm_lasso_args {
   double* u;
   double* W0;              /* [dev] u - alpha on entry; W1 scratch (ping-pong)                 */
   double* W1;
-  double* partial;         /* [dev] >= ipm_lasso_partial_doubles(n, S)                         */
+  double* partial;         /* [dev] >= ipm_lasso_partial_doubles(n, S), zeroed once before use  */
   double rho, eps_abs, eps_rel, stop_multiplier;
   int32_t max_iters, check_stop;
   int32_t positive, add_bias;

@@ -2330,12 +2330,77 @@ void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64
   trsm_lower_bwd(st, n, nrhs, L, ldl, W, ldb, B);
 }
 
-// =====================================================================================
-// LU with partial pivoting (column-major A, in place), right-looking, one column per step.
-// Fallback path only (after a Cholesky failure).  A zero pivot column is recorded with
-// piv = -1 - row and skipped; getrs then sets that unknown to 0 (the minimum-norm choice
-// when the null space is that coordinate -- see DESIGN.md, fallback semantics).
-// =====================================================================================
+// ---- many right-hand sides: L L^T X = B in 128-row blocks on fp64 MFMA GEMMs (the Lasso's
+// cho_solve(., I), LassoSolver.py:178-189; the per-column substitution kernels above take seconds
+// at n = 4096 with n right-hand sides).  B row-major n x nrhs.  With Xs_j = L_jj^-T (k_trinv128,
+// row-major 128 x 128: as a k-major operand it is L_jj^-1) and its transpose XsT_j (= L_jj^-T as a
+// k-major operand):
+//   forward  Y_j = L_jj^-1 B_j;            B_i -= L_ij Y_j        (i > j; L columns are k-major)
+//   backward X_j = L_jj^-T Y_j;            B_i -= L_ji^T X_j      (i < j; rows of L: the row-major
+//                                                                   copy Lr, k-major)
+// Every product is C(s, r) = sum_k X[k][s] Y[k][r] of the MFMA tile with C = the row-major block.
+__global__ void k_block_transpose128(int64_t nblk, const double* __restrict__ in, double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nblk * 16384) return;
+  const int64_t b = e >> 14, q = e & 16383, r = q >> 7, c = q & 127;
+  out[(b << 14) + c * 128 + r] = in[(b << 14) + r * 128 + c];
+}
+__global__ void k_copy_rows(int64_t rows, int64_t cols, const double* __restrict__ in, int64_t ldi,
+                            double* __restrict__ out, int64_t ldo) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rows * cols) return;
+  const int64_t r = e / cols, c = e - r * cols;
+  out[r * ldo + c] = in[r * ldi + c];
+}
+int64_t potrs_blocked_ws_doubles(int64_t n, int64_t nrhs) {
+  const int64_t nblk = cdiv(n, 128);
+  return 2 * nblk * 16384 + n * n + 128 * nrhs + 64;
+}
+void potrs_blocked(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B, int64_t ldb,
+                   double* ws) {
+  if (n <= 0 || nrhs <= 0) return;
+  const int64_t nblk = cdiv(n, 128);
+  double* Xs = ws;
+  double* XsT = Xs + nblk * 16384;
+  double* Lr = XsT + nblk * 16384;
+  double* T = Lr + n * n;
+  hipLaunchKernelGGL(k_trinv128, dim3((unsigned)nblk), dim3(512), 0, st, n, L, ldl, Xs);
+  hipLaunchKernelGGL(k_block_transpose128, dim3((unsigned)cdiv(nblk * 16384, 256)), dim3(256), 0, st, nblk, Xs, XsT);
+  transpose(st, n, n, L, ldl, Lr, n);   // Lr[r * n + c] = L(r, c)
+  auto gemm = [&](int64_t ni, int64_t nj, int64_t K, const double* X, int64_t ldx, const double* Y, int64_t ldy,
+                  double* C, int64_t ldc, bool sub) {
+    if (ni <= 0 || nj <= 0 || K <= 0) return;
+    GemmArgs g;
+    g.ni = ni;
+    g.nj = nj;
+    g.K = K;
+    g.X = X;
+    g.ldx = ldx;
+    g.Y = Y;
+    g.ldy = ldy;
+    g.C = C;
+    g.ldc = ldc;
+    g.sub = sub ? 1 : 0;
+    mfma_gemm_launch(st, g);
+  };
+  auto diag = [&](int64_t j, const double* Yblk) {   // B_j <- inv-block * B_j (through T)
+    const int64_t j0 = j * 128, bj = std::min<int64_t>(128, n - j0);
+    gemm(nrhs, bj, bj, B + j0 * ldb, ldb, Yblk, 128, T, nrhs, false);
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)cdiv(bj * nrhs, 256)), dim3(256), 0, st, bj, nrhs, T, nrhs,
+                       B + j0 * ldb, ldb);
+  };
+  for (int64_t j = 0; j < nblk; ++j) {
+    const int64_t j0 = j * 128, j1 = std::min<int64_t>(n, j0 + 128);
+    diag(j, Xs + j * 16384);
+    gemm(nrhs, n - j1, j1 - j0, B + j0 * ldb, ldb, L + j0 * ldl + j1, ldl, B + j1 * ldb, ldb, true);
+  }
+  for (int64_t j = nblk - 1; j >= 0; --j) {
+    const int64_t j0 = j * 128, j1 = std::min<int64_t>(n, j0 + 128);
+    diag(j, XsT + j * 16384);
+    gemm(nrhs, j0, j1 - j0, B + j0 * ldb, ldb, Lr + j0 * n, n, B, ldb, true);
+  }
+}
+
 // ---- LU with partial pivoting (np.linalg.solve; the Cholesky fallback, Q9), column-major.
 // Blocked right-looking: panels of LU_NB columns are factored column by column (pivot search,
 // swap and scale in one workgroup; the rank-1 update restricted to the panel), then the panel's

@@ -122,6 +122,11 @@ void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H,
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                  int64_t ldb, double* W, unsigned* ctl, double* xinv_ws = nullptr);
+// L L^T X = B for many right-hand sides (nrhs >~ 32): 128-row blocks on MFMA GEMMs; ws of
+// potrs_blocked_ws_doubles(n, nrhs) doubles
+int64_t potrs_blocked_ws_doubles(int64_t n, int64_t nrhs);
+void potrs_blocked(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B, int64_t ldb,
+                   double* ws);
 // L^T x = b, one right-hand side read with stride bstride; ctl: 2 device words
 // xinv_ws: trsv_inv_ws_doubles(n) doubles for the inverted 128 x 128 diagonal blocks (null: the
 // 64-row substitution kernel)

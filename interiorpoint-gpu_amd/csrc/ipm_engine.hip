@@ -541,6 +541,13 @@ extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double
 extern "C" int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
                          int64_t ldb) {
   if (!h || n < 0 || nrhs < 0 || ldl < n || ldb < nrhs) return IPM_INVALID_ARG;
+  if (nrhs >= 32 && n >= 128) {
+    double* W = scratch(h, potrs_blocked_ws_doubles(n, nrhs) * sizeof(double));
+    if (!W) return IPM_HIP_ERROR;
+    potrs_blocked(h->stream, n, nrhs, L, ldl, B, ldb, W);
+    HIPCHK(h, hipGetLastError());
+    return IPM_OK;
+  }
   const int64_t wn = (std::max<int64_t>(n * ldb, 1) + 31) & ~int64_t(31);
   double* W = scratch(h, (wn + trsv_inv_ws_doubles(n)) * sizeof(double));
   if (!W) return IPM_HIP_ERROR;

@@ -47,6 +47,8 @@ struct AdmmStep {
   double* alpha = nullptr;
   double* u = nullptr;
   double* partial = nullptr;    // 4 doubles per tile (check iterations)
+  double* kpart = nullptr;      // K-split partial tiles: (tile * ks + z) * LT * LT
+  unsigned* kcnt = nullptr;     // K-split arrivals per tile (the last one finishes the tile, resets it)
   double rho = 0.0;
   int ba_bcast = 0, eta_bcast = 0, positive = 0, add_bias = 0, dual_form = 0;
 };
@@ -66,6 +68,10 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
   }
   const double* qp = a.Qs + i0 + fr;
   const double* wp = W + s0 + fr;
+  // K split over gridDim.z workgroups (z-th chunk of 16-row multiples)
+  const int KS = gridDim.z, z = blockIdx.z;
+  const int64_t kchunk = ((n + 16 * KS - 1) / (16 * KS)) * 16;
+  const int64_t kbeg = z * kchunk, kend = min(n, kbeg + kchunk);
   dbl4 acc[2][2];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -74,12 +80,12 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
   // wave wv takes the 4-row slabs kb = 4 wv + 16 j; lane row k = kb + fk.  Four slabs per pass:
   // 16 independent loads in flight before the 16 MFMAs that consume them.
   constexpr int U = 4;
-  for (int64_t kb = 4 * wv; kb < n; kb += 16 * U) {
+  for (int64_t kb = kbeg + 4 * wv; kb < kend; kb += 16 * U) {
     double av[U][2], bv[U][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t k = kb + 16 * u + fk;
-      const bool kin = k < n;
+      const bool kin = k < kend;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         av[u][t] = (kin && iin[t]) ? qp[k * ldq + 16 * t] : 0.0;
@@ -101,14 +107,41 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wv][(16 * p + fk + 4 * r) * (LT + 1) + 16 * q + fr] = acc[p][q][r];
   __syncthreads();
+  double qv[4];
+#pragma unroll
+  for (int e4 = 0; e4 < 4; ++e4) {
+    const int e = tid + 256 * e4, o = (e >> 5) * (LT + 1) + (e & 31);
+    qv[e4] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+  }
+  if (KS > 1) {
+    // hand the partial tile over; the last of the KS workgroups of this tile sums all of them in
+    // split order (deterministic) and runs the epilogue
+    const int64_t tile = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    double* mine = a.kpart + (tile * KS + z) * (LT * LT);
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) st_sc1(&mine[tid + 256 * e4], qv[e4]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int last;
+    if (tid == 0)
+      last = __hip_atomic_fetch_add(&a.kcnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(KS - 1);
+    __syncthreads();
+    if (!last) return;
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      double t = 0.0;
+      for (int q = 0; q < KS; ++q) t += ld_sc1(&a.kpart[(tile * KS + q) * (LT * LT) + tid + 256 * e4]);
+      qv[e4] = t;
+    }
+    if (tid == 0) __hip_atomic_store(&a.kcnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   double pr = 0.0, pd = 0.0, pa = 0.0, pu = 0.0;
 #pragma unroll
   for (int e4 = 0; e4 < 4; ++e4) {
     const int e = tid + 256 * e4, il = e >> 5, sl = e & 31;
     const int64_t i = i0 + il, s = s0 + sl;
     if (i < n && s < S) {
-      const int o = il * (LT + 1) + sl;
-      const double qw = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+      const double qw = qv[e4];
       const int64_t ix = i * lds + s;
       const double xv = a.bA[i * a.ldba + (a.ba_bcast ? 0 : s)] + qw;   // bA + Qs (u - alpha)
       const double uo = a.u[ix], ao = a.alpha[ix];
@@ -361,8 +394,20 @@ extern "C" int ipm_lasso_loss(ipm_handle* h, const ipm_lasso_args* a, int absm, 
   return IPM_OK;
 }
 
+// K split of the iteration GEMM: enough workgroups for the chip (>= ~512), chunks of >= 128 rows
+static int admm_ksplit(int64_t n, int64_t S) {
+  const int64_t tiles = ((S + LT - 1) / LT) * ((n + LT - 1) / LT);
+  int64_t ks = (512 + tiles - 1) / tiles;
+  ks = std::min<int64_t>(ks, std::max<int64_t>(n / 128, 1));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ks, 8));
+}
+
+// [norm partials: 4 per tile + 8][K-split partial tiles][K-split counters (as doubles)]; must be
+// zero-initialised once (the counters reset themselves)
 extern "C" int64_t ipm_lasso_partial_doubles(int64_t n, int64_t S) {
-  return 4 * ((S + LT - 1) / LT) * ((n + LT - 1) / LT) + 8;
+  const int64_t tiles = ((S + LT - 1) / LT) * ((n + LT - 1) / LT);
+  const int ks = admm_ksplit(n, S);
+  return 4 * tiles + 8 + (ks > 1 ? tiles * ks * LT * LT + tiles : 0);
 }
 
 extern "C" int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* iters) {
@@ -392,9 +437,14 @@ extern "C" int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* i
   s.positive = a->positive;
   s.add_bias = a->add_bias;
   s.dual_form = a->dual_form;
-  const dim3 grid((unsigned)((a->S + LT - 1) / LT), (unsigned)((a->n + LT - 1) / LT));
+  const int ks = admm_ksplit(a->n, a->S);
+  const dim3 grid((unsigned)((a->S + LT - 1) / LT), (unsigned)((a->n + LT - 1) / LT), (unsigned)ks);
   const int64_t nblk = (int64_t)grid.x * grid.y;
   double* norms = a->partial + 4 * nblk;
+  if (ks > 1) {
+    s.kpart = a->partial + 4 * nblk + 8;
+    s.kcnt = reinterpret_cast<unsigned*>(s.kpart + nblk * ks * LT * LT);
+  }
   double* W = a->W0;
   double* Wn = a->W1;
   int it = 0;

@@ -150,7 +150,7 @@ class LassoSolver:
         import torch
         z = lambda: torch.zeros((self.n, S), dtype=torch.float64, device=self.dev)  # noqa: E731
         st = dict(x=z(), alpha=z(), u=z(), W0=z(), W1=z(),
-                  partial=torch.empty(int(self.lib.ipm_lasso_partial_doubles(self.n, S)), dtype=torch.float64,
+                  partial=torch.zeros(int(self.lib.ipm_lasso_partial_doubles(self.n, S)), dtype=torch.float64,
                                       device=self.dev),
                   eta=_dev(np.atleast_1d(eta), self.dev), reg=_dev(np.atleast_1d(reg), self.dev))
         a = LassoArgs()

@@ -196,3 +196,27 @@ def test_getrf_getrs_match_numpy(n):
     assert h.lib.ipm_getrs(h.ptr, n, 2, L.dptr(Ad), n, L.dptr(piv), L.dptr(Bd), 2) == 0
     ref = np.linalg.solve(A, b)
     np.testing.assert_allclose(Bd.cpu().numpy(), ref, rtol=1e-8, atol=1e-10 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("n,nrhs", [(130, 40), (1030, 300), (2100, 64), (4097, 4097)])
+def test_potrs_many_rhs_blocked(n, nrhs):
+    """L L^T X = B with many right-hand sides (128-row blocks on MFMA GEMMs, the Lasso's Q = M^-1)
+    against torch's Cholesky solve."""
+    import torch
+    from gpu_util import potrf as P
+    from gpu_util import handle
+    from ipm355 import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(n)
+    M = torch.rand((n + 5, n), dtype=torch.float64, device="cuda", generator=g) - 0.5
+    A = M.T @ M + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    H = A.clone()
+    rc, info = P(H, n, n)
+    assert rc == 0 and info == 0
+    B = torch.rand((n, nrhs), dtype=torch.float64, device="cuda", generator=g) - 0.5
+    X = B.clone()
+    h = handle()
+    assert h.lib.ipm_potrs(h.ptr, n, nrhs, L.dptr(H), n, L.dptr(X), nrhs) == 0
+    ref = torch.cholesky_solve(B, torch.linalg.cholesky(A))
+    err = ((X - ref).abs().max() / ref.abs().max()).item()
+    print(f"n={n} nrhs={nrhs}: max rel {err:.2e}")
+    assert err < 1e-10
