@@ -1005,7 +1005,14 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     potrf_lower_la(st, &pr->h->pst, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
-    potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
+    if (p >= 32 && n >= 128) {
+      // many right-hand sides: 128-row blocks on MFMA GEMMs (handle scratch, grown on demand)
+      double* bw = scratch(pr->h, (size_t)potrs_blocked_ws_doubles(n, p) * sizeof(double));
+      if (!bw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+      potrs_blocked(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, bw);
+    } else {
+      potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
+    }
     copy(st, pr->tmpn, pr->g, n);
     potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl, pr->xinv);
     // S = A Y (lower)

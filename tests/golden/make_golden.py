@@ -331,6 +331,17 @@ def npy_lp():
                                                  get_dual_variables=True))
 
 
+def eq_many():
+    """Dense infeasible-start Cholesky with many equality rows (block elimination with H^-1 A^T over
+    p = 40 right-hand sides, NewtonSolverInfeasibleStart.py:386-511): the blocked multi-RHS solve."""
+    rng = np.random.default_rng(21)
+    n, p = 256, 40
+    pr = problems.qp_ineq_box(n, 64, seed=21, with_xf=True)
+    xf = pr.pop("xf")
+    Aeq = rng.uniform(-2, 2, (p, n))
+    run_solve("qp_eq_many", RefQP, dict(pr, A=Aeq, b=Aeq @ xf, **problems.QP_KWARGS))
+
+
 def extra():
     """Round-2 fixtures: the remaining solve classes pinned by the reference itself."""
     # feasible NewtonSolverDiagonal: LP with bounds only, no C, no A (LPSolver.py:436-446 dispatch)
@@ -365,6 +376,8 @@ if __name__ == "__main__":
     _wrap_feasible()
     if sys.argv[1:] == ["extra"]:
         extra()
+    elif sys.argv[1:] == ["eq_many"]:
+        eq_many()
     elif sys.argv[1:] == ["npy_lp"]:
         npy_lp()
     elif sys.argv[1:] == ["eq_box_stable"]:

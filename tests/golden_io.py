@@ -15,6 +15,7 @@ SOLVE_CASES = {
     "lp_eq_box_tk1": "LP", "lp_eq_box_tk2": "LP", "lp_eq_box_tk1_us5": "LP",
     # LPs in the reference's sequential .npy format, get_dual_variables=True
     "lp_npy_miplib": "LP", "lp_ineq_box_duals": "LP", "lp_eq_box_tk1_duals": "LP",
+    "qp_eq_many": "QP",
 }
 
 # linear_solve_method np_solve / np_lstsq / direct, pinned by the reference (make_golden.py extra)
