@@ -89,6 +89,13 @@ EXPORTS = {
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),
+    # batch group (config 4)
+    "ipm_batch_create": (C.c_int, [F64, C.POINTER(P)]),
+    "ipm_batch_destroy": (C.c_int, [P]),
+    "ipm_batch_join": (C.c_int, [P]),
+    "ipm_batch_leave": (C.c_int, [P]),
+    "ipm_batch_stats": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
+    "ipm_problem_set_batch": (C.c_int, [P, P]),
     # batched ADMM Lasso (ipm_lasso.hip; ipm355/lasso.py)
     "ipm_gemm_tn": (C.c_int, [P, I64, I64, I64, F64, P, I64, P, I64, F64, P, I64]),
     "ipm_transpose": (C.c_int, [P, I64, I64, P, I64, P, I64]),
@@ -117,7 +124,10 @@ def load_library(path: str = LIB_PATH):
         lib = C.CDLL(path)
     except OSError as e:
         raise IPMBackendError(f"cannot load {path}: {e}") from e
+    default = os.path.join(_HERE, "libipm355.so")
     for name, (res, args) in EXPORTS.items():
+        if path != default and not hasattr(lib, name):
+            continue          # an older build under IPM355_LIB (A/B experiments): only what it has
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
