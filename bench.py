@@ -189,9 +189,6 @@ def main():
                     help="which phase(s) the timed steps run in (default: half each)")
     ap.add_argument("--concurrent", action="store_true",
                     help="solve the instances concurrently: one HIP stream + host thread each")
-    ap.add_argument("--batch", action="store_true",
-                    help="with --concurrent: a batch group -- the instances' Newton-step Cholesky factorisations "
-                         "run as one grid (ipm355.batch)")
     ap.add_argument("--problem", choices=["qp", "lp", "socp"], default="qp",
                     help="qp: the headline M3-QP (default); lp: M3-LP (config 3); socp: M5, --m = cones (config 5)")
     ap.add_argument("--instances", type=int, default=1,
@@ -265,7 +262,6 @@ def main():
         h = L.Handle.get(dev_index)
     import ctypes
     res = {}
-    batch_stats = None
     for name, budget in segs:
         if budget <= 0:
             res[name] = dict(iters=0, seconds=0.0, kkt_ms=0.0, potrf_ms=0.0, kkt_flops=0.0, N=0)
@@ -283,20 +279,12 @@ def main():
         t0 = time.perf_counter()
         if args.concurrent:
             from concurrent.futures import ThreadPoolExecutor
-            group = None
-            if args.batch:
-                from ipm355.batch import BatchGroup
-                group = BatchGroup()
-                for sv in solvers:
-                    group.attach(sv)
 
             def run(k):
-                with on(streams[k]), (group.member() if group is not None else contextlib.nullcontext()):
+                with on(streams[k]):
                     solvers[k].solve(iteration_budget=budget)
             with ThreadPoolExecutor(max_workers=len(solvers)) as ex:
                 list(ex.map(run, range(len(solvers))))
-            if group is not None:
-                batch_stats = group.stats()
         else:
             for s in solvers:
                 s.solve(iteration_budget=budget)
@@ -358,8 +346,7 @@ def main():
                                    f"instance {k1} phase-1 iterations (from x0=0) + {args.steps - k1} barrier-phase "
                                    f"iterations (from the feasible x_f); {args.instances} independent instance(s) "
                                    f"per GPU" + (" solved concurrently (one stream + host thread each)"
-                                                 if args.concurrent else "")
-                                   + (", Newton-step Cholesky factorisations batched into one grid" if args.batch else ""),
+                                                 if args.concurrent else ""),
                        "n": n, "m": m, "instances_per_gpu": args.instances,
                        "parallelism": f"instances{world * args.instances}", "backend": backend if world > 1 else None},
             "phases": {nm: {"iters": per[nm]["iters"], "seconds_max_rank": per[nm]["tmax"],
@@ -393,8 +380,6 @@ def main():
             "newton_iters": total_iters,
             "lib_sha256": lib_digest(),
         }
-        if batch_stats is not None:
-            rec["batch_group"] = {"leader_launches": batch_stats[0], "member_factorisations": batch_stats[1]}
         if args.problem != "qp":
             rec["metric"] = f"Newton iters/sec, dense {args.problem.upper()} (config {'3' if args.problem == 'lp' else '5'})"
             rec["config"]["workload"] = rec["config"]["workload"].replace("QPSolver", Cls.__name__).replace(

@@ -153,18 +153,6 @@ int ipm_problem_destroy(ipm_problem* pr);
    updated in place (Q8); v [dev] (p) likewise; t is the barrier parameter. */
 int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v, const ipm_newton_opts* opts,
                      ipm_newton_result* res);
-/* Batch group: independent problems solved concurrently (one host
-   thread and stream each) meet at every Newton-step Cholesky; one member launches the
-   factorisations of all that arrived as ONE grid (same size; at most 16).  A member that does not
-   arrive within timeout_us (it is elsewhere: phase change, LU fallback, finished) is not waited for.
-   join/leave bracket a member's solve; stats: leader launches and member factorisations batched. */
-typedef struct ipm_batch ipm_batch;
-int ipm_batch_create(double timeout_us, ipm_batch** out);
-int ipm_batch_destroy(ipm_batch* b);
-int ipm_batch_join(ipm_batch* b);
-int ipm_batch_leave(ipm_batch* b);
-int ipm_batch_stats(ipm_batch* b, int64_t* launches, int64_t* batched);
-int ipm_problem_set_batch(ipm_problem* pr, ipm_batch* b);   /* NULL: not batched */
 /* persistent Cholesky-failure flag (Q9) */
 int ipm_get_use_backup(ipm_problem* pr);
 int ipm_set_use_backup(ipm_problem* pr, int flag);

@@ -933,13 +933,6 @@ struct BlockArgs {
   int64_t s_full = 0;
   double* sscr = nullptr;       // split p's upper-half partial tile at sscr + p * 128 * 128
   unsigned* sflag = nullptr;    // split p done: sflag[p]
-  // batch of independent factorisations of the same size in ONE grid (config 4): workgroup w
-  // belongs to instance w % nbatch; every pointer above is instance 0's, instance i's are offset by
-  // bdA[i] (A-derived, doubles), bdW[i] (workspace-derived, doubles) and bdI[i] (info, ints).  Each
-  // instance has its own control words, so tickets and hand-offs stay per instance.
-  static constexpr int MAXB = 16;
-  int nbatch = 1;
-  int64_t bdA[MAXB] = {}, bdW[MAXB] = {}, bdI[MAXB] = {};
 };
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
@@ -1017,8 +1010,8 @@ struct RoleTrace {
 #define ROLE(r) ((void)0)
 #endif
 
-template <bool VEC, bool BATCH>
-__device__ __forceinline__ void potrf_block_body(const BlockArgs& b, const BlockArgs& bargs) {
+template <bool VEC>
+__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ BlockSmem sm;
   __shared__ int sticket, sflag;
   const int tid = threadIdx.x;
@@ -1309,17 +1302,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, const Block
     if (tid == 0) {
       if (b.s_map == 2) t = xcd_tile(&b.ctl[CTL_XQ], b.ns);   // this workgroup's tile: its XCD's run
       const unsigned me = 1u + cu_key();
-      if (BATCH) {
-        // batched grid: never beside ANOTHER instance's diagonal role either -- hold the slot
-        // (keeping MFMA work off that CU) until it is done
-#pragma unroll
-        for (int j = 0; j < BlockArgs::MAXB; ++j) {
-          if (j >= bargs.nbatch) break;
-          unsigned* cj = bargs.ctl + 2 * bargs.bdW[j];
-          if (cj == b.ctl) continue;
-          while (ld_ctl(&cj[CTL_CRIT]) == me || ld_ctl(&cj[CTL_CRIT + NCRIT - 1]) == me) __builtin_amdgcn_s_sleep(20);
-        }
-      }
       int q = -1;
       for (int i = 0; i < NCRIT && q < 0; ++i)
         if (ld_ctl(&b.ctl[CTL_CRIT + i]) == me) q = i;
@@ -1352,44 +1334,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, const Block
       }
     }
   }
-}
-
-// one launch per 256-column block; the batched form (config 4): the grid holds nbatch instances
-// (workgroup w -> instance w % nbatch), each with its own pointers and control words
-template <bool VEC>
-__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) { potrf_block_body<VEC, false>(b, b); }
-
-template <bool VEC>
-__global__ __launch_bounds__(256, 2) void k_potrf_block_batch(BlockArgs bargs) {
-  BlockArgs b = bargs;
-  {
-    // this workgroup's instance: constant-index selects (a dynamically indexed kernel-argument
-    // array would put the whole argument block in scratch memory)
-    const int inst = __builtin_amdgcn_readfirstlane((int)(blockIdx.x % (unsigned)bargs.nbatch));
-    int64_t dA = 0, dW = 0, dI = 0;
-#pragma unroll
-    for (int i = 0; i < BlockArgs::MAXB; ++i)
-      if (i == inst) { dA = bargs.bdA[i]; dW = bargs.bdW[i]; dI = bargs.bdI[i]; }
-    auto rfl64 = [](int64_t v) {   // wave-uniform 64-bit value into scalar registers
-      const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
-      const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
-      return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
-    };
-    dA = rfl64(dA);
-    dW = rfl64(dW);
-    dI = rfl64(dI);
-    b.A += dA;
-    b.info += dI;
-    b.wsA += dW;
-    b.wsB += dW;
-    b.ctl += 2 * dW;
-    b.prevfail += 2 * dW;
-    b.la32.X += dA; b.la32.Y += dA; b.la32.C += dA;
-    b.la.X += dA; b.la.Y += dA; b.la.C += dA;
-    b.la128.X += dA; b.la128.Y += dA; b.la128.C += dA;
-    b.s.X += dA; b.s.Y += dA; b.s.C += dA;
-  }
-  potrf_block_body<VEC, true>(b, bargs);
 }
 
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
@@ -1449,13 +1393,7 @@ static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64
 }
 
 void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
-                       const DeferSyrk* ds, int nbatch, double* const* Ab, int* const* infob, double* const* wsb) {
-  if (nbatch > 1) {
-    ds = nullptr;
-    A = Ab[0];
-    info = infob[0];
-    ws = wsb[0];
-  }
+                       const DeferSyrk* ds) {
   const bool defer = ds && ds->active();
   if (ncols < 0 || ncols > n) ncols = n;
   if (ncols <= 0) {
@@ -1465,11 +1403,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
   // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
-  for (int i = 0; i < nbatch; ++i) {
-    int* inf = nbatch > 1 ? infob[i] : info;
-    double* wsi = nbatch > 1 ? wsb[i] : ws;
-    zero2(st, inf, 1, reinterpret_cast<unsigned*>(wsi + 2 * PANEL_WS), 8 + nblocks * cw);
-  }
+  zero2(st, info, 1, ctl0, 8 + nblocks * cw);
   const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
   // IPM_RAG=0: ragged trailing rows as a row of 128-tiles (read per call: tests compare both)
   const char* erag = getenv("IPM_RAG");
@@ -1596,7 +1530,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
     }
-    if (b.ns > 0 && !defer && split_on && nbatch == 1) {
+    if (b.ns > 0 && !defer && split_on) {
       // the planner's split count (cached per size and block: it depends on nothing else)
       static std::mutex mu;
       static std::map<std::pair<int64_t, int64_t>, std::vector<int64_t>> cache;
@@ -1644,23 +1578,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       }
       b.gs_total = b.gs_cum[b.ngs];
     }
-    int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
-    if (nbatch > 1) {
-      b.nbatch = nbatch;
-      for (int i = 0; i < nbatch; ++i) {
-        b.bdA[i] = Ab[i] - Ab[0];
-        b.bdW[i] = wsb[i] - wsb[0];
-        b.bdI[i] = infob[i] - infob[0];
-      }
-      grid *= nbatch;
-    }
-    if (nbatch > 1) {
-      if (vec) hipLaunchKernelGGL(k_potrf_block_batch<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
-      else hipLaunchKernelGGL(k_potrf_block_batch<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
-    } else {
-      if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
-      else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
-    }
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
+    if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
   }
 }
 

@@ -106,12 +106,8 @@ int defer_ks();   // k rows per deferred slice (IPM_DEFER_KS, default 256)
 // one launch per 256-column block on stream s (the default behind potrf_lower / potrf_lower_la).
 // ncols < n: only the first ncols columns are factored (all n rows) -- the bordered Newton system
 // needs row n-1 of L (the forward-solved right-hand side) but not its diagonal entry.
-inline int BlockArgs_MAXB() { return 16; }   // largest batch of one fused Cholesky grid
-// nbatch > 1: the factorisations of nbatch independent matrices of the same (n, ldh, ncols) in one
-// launch sequence, instance i's (H, info, ws) = (Hb[i], infob[i], wsb[i]) (H / info / ws ignored)
 void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws,
-                       int64_t ncols = -1, const DeferSyrk* ds = nullptr, int nbatch = 1, double* const* Hb = nullptr,
-                       int* const* infob = nullptr, double* const* wsb = nullptr);
+                       int64_t ncols = -1, const DeferSyrk* ds = nullptr);
 // default: potrf_lower_fused on s.  IPM_POTRF_LA=1: the earlier two-stream form -- panels on
 // ps->side (high priority), trailing updates on ps->main, events between them (ps == null or
 // ps->side == null: everything in order on s; ncols is ignored there).  The call is ordered

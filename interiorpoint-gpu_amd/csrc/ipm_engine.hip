@@ -18,10 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <condition_variable>
 #include <cstring>
-#include <chrono>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,34 +54,6 @@ enum Slot {
   SC_COUNT
 };
 }  // namespace
-
-// Batch group (config 4: independent instances solved concurrently, one host thread + stream each):
-// members meet at every Newton-step Cholesky and ONE of them launches the factorisations of all
-// that arrived (same size: one grid, potrf_lower_fused with nbatch > 1; critical-path roles of all
-// instances dispatched first).  A member that is elsewhere (phase change, LU fallback, finished)
-// is not waited for longer than `timeout`.
-struct BatchReq {
-  ipm_problem* pr;
-  int64_t n, ldh, ncols;
-  double* H;
-  int* info;
-  double* ws;
-  hipEvent_t ready;
-};
-struct ipm_batch {
-  std::mutex mu;
-  std::condition_variable cv;
-  int active = 0;
-  double timeout_us = 300.0;
-  uint64_t round = 0;                  // requests of round r are launched by its leader
-  std::vector<BatchReq> reqs;
-  static constexpr int NEV = 64;
-  hipEvent_t done[NEV] = {};
-  uint64_t pub[NEV];                   // pub[r % NEV] == r: round r's done event is recorded
-  int err = IPM_OK;                    // a leader's launch error, reported to its round's members
-  ipm_batch() { for (auto& p : pub) p = ~uint64_t(0); }
-  int64_t launches = 0, batched = 0;   // statistics: leader launches, member factorisations batched
-};
 
 struct ipm_problem {
   ipm_handle* h = nullptr;
@@ -123,8 +92,6 @@ struct ipm_problem {
   double* Gd = nullptr;
   DeferSyrk dsy;
   bool defer_on = false;
-  ipm_batch* batch = nullptr;   // batch group (config 4), or null
-  hipEvent_t bready = nullptr;  // this member's "H is assembled" event
 };
 
 // ------------------------------------------------------------------------- workspace
@@ -735,55 +702,7 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
 }
 
 extern "C" int ipm_problem_destroy(ipm_problem* pr) {
-  if (pr && pr->bready) hipEventDestroy(pr->bready);
   delete pr;
-  return IPM_OK;
-}
-
-extern "C" int ipm_batch_create(double timeout_us, ipm_batch** out) {
-  if (!out) return IPM_INVALID_ARG;
-  ipm_batch* b = new ipm_batch();
-  b->timeout_us = timeout_us > 0 ? timeout_us : 300.0;
-  for (auto& e : b->done)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { delete b; return IPM_HIP_ERROR; }
-  *out = b;
-  return IPM_OK;
-}
-
-extern "C" int ipm_batch_destroy(ipm_batch* b) {
-  if (!b) return IPM_OK;
-  for (auto& e : b->done) if (e) hipEventDestroy(e);
-  delete b;
-  return IPM_OK;
-}
-
-extern "C" int ipm_batch_join(ipm_batch* b) {
-  if (!b) return IPM_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(b->mu);
-  ++b->active;
-  return IPM_OK;
-}
-
-extern "C" int ipm_batch_leave(ipm_batch* b) {
-  if (!b) return IPM_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(b->mu);
-  --b->active;
-  b->cv.notify_all();   // members waiting for this one stop waiting
-  return IPM_OK;
-}
-
-extern "C" int ipm_batch_stats(ipm_batch* b, int64_t* launches, int64_t* batched) {
-  if (!b) return IPM_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(b->mu);
-  if (launches) *launches = b->launches;
-  if (batched) *batched = b->batched;
-  return IPM_OK;
-}
-
-extern "C" int ipm_problem_set_batch(ipm_problem* pr, ipm_batch* b) {
-  if (!pr) return IPM_INVALID_ARG;
-  if (b && !pr->bready) HIPCHK(pr->h, hipEventCreateWithFlags(&pr->bready, hipEventDisableTiming));
-  pr->batch = b;
   return IPM_OK;
 }
 
@@ -1014,71 +933,6 @@ static int expand_full_inplace(ipm_problem* pr, double* M, int64_t n, int64_t ld
 
 namespace {
 
-// the Newton-step Cholesky through the batch group (see ipm_batch)
-int batch_potrf(ipm_problem* pr, double* H, int64_t n, int64_t ldh, int64_t ncols) {
-  ipm_batch& B = *pr->batch;
-  hipStream_t st = S(pr);
-  ipm_handle* h = pr->h;
-  HIPCHK(h, hipEventRecord(pr->bready, st));
-  std::unique_lock<std::mutex> lk(B.mu);
-  const uint64_t my = B.round;
-  B.reqs.push_back(BatchReq{pr, n, ldh, ncols, H, pr->info, pr->pws, pr->bready});
-  B.cv.notify_all();
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds((int64_t)B.timeout_us);
-  B.cv.wait_until(lk, deadline, [&] { return B.round != my || (int)B.reqs.size() >= B.active; });
-  if (B.round == my) {
-    // leader: launch everything that arrived this round, on this member's stream
-    std::vector<BatchReq> rq;
-    rq.swap(B.reqs);
-    ++B.round;
-    lk.unlock();
-    auto launch = [&]() -> hipError_t {
-      for (const auto& r : rq)
-        if (r.pr != pr) {
-          const hipError_t e = hipStreamWaitEvent(st, r.ready, 0);
-          if (e != hipSuccess) return e;
-        }
-      std::vector<bool> done(rq.size(), false);
-      for (size_t i = 0; i < rq.size(); ++i) {
-        if (done[i]) continue;
-        std::vector<double*> Hs, Ws;
-        std::vector<int*> Is;
-        for (size_t j = i; j < rq.size() && (int)Hs.size() < BlockArgs_MAXB(); ++j)
-          if (!done[j] && rq[j].n == rq[i].n && rq[j].ldh == rq[i].ldh && rq[j].ncols == rq[i].ncols) {
-            Hs.push_back(rq[j].H);
-            Is.push_back(rq[j].info);
-            Ws.push_back(rq[j].ws);
-            done[j] = true;
-          }
-        if (Hs.size() == 1)
-          potrf_lower_fused(st, rq[i].n, Hs[0], rq[i].ldh, Is[0], Ws[0], rq[i].ncols);
-        else
-          potrf_lower_fused(st, rq[i].n, nullptr, rq[i].ldh, nullptr, nullptr, rq[i].ncols, nullptr, (int)Hs.size(),
-                            Hs.data(), Is.data(), Ws.data());
-      }
-      const hipError_t e = hipEventRecord(B.done[my % ipm_batch::NEV], st);
-      return e != hipSuccess ? e : hipGetLastError();
-    };
-    const hipError_t e = launch();
-    lk.lock();
-    // always publish (members of this round must not wait forever, even after an error)
-    B.pub[my % ipm_batch::NEV] = my;
-    if (e != hipSuccess) B.err = IPM_HIP_ERROR;
-    B.launches += 1;
-    B.batched += (int64_t)rq.size();
-    B.cv.notify_all();
-    if (e != hipSuccess) { h->err = hipGetErrorString(e); return IPM_HIP_ERROR; }
-    return IPM_OK;
-  }
-  // follower: wait for this round's leader to publish, then order this stream after it
-  B.cv.wait(lk, [&] { return B.pub[my % ipm_batch::NEV] == my; });
-  if (B.err != IPM_OK) { h->err = "batch leader failed to launch"; return IPM_HIP_ERROR; }
-  hipEvent_t ev = B.done[my % ipm_batch::NEV];
-  lk.unlock();
-  HIPCHK(h, hipStreamWaitEvent(st, ev, 0));
-  return IPM_OK;
-}
-
 // dense feasible direction on the Cholesky path; LU if use_backup.
 int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
   hipStream_t st = S(pr);
@@ -1098,12 +952,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
     // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
-    if (pr->batch && !defer) {
-      const int rc = batch_potrf(pr, pr->H, pr->N + 1, pr->ldh, pr->N);
-      if (rc) return rc;
-    } else {
-      potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
-    }
+    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
     if (h->timing) hipEventRecord(h->ev[3], st);
     trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv);
   } else {

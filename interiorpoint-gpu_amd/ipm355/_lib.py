@@ -89,13 +89,6 @@ EXPORTS = {
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),
-    # batch group (config 4)
-    "ipm_batch_create": (C.c_int, [F64, C.POINTER(P)]),
-    "ipm_batch_destroy": (C.c_int, [P]),
-    "ipm_batch_join": (C.c_int, [P]),
-    "ipm_batch_leave": (C.c_int, [P]),
-    "ipm_batch_stats": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
-    "ipm_problem_set_batch": (C.c_int, [P, P]),
     # batched ADMM Lasso (ipm_lasso.hip; ipm355/lasso.py)
     "ipm_gemm_tn": (C.c_int, [P, I64, I64, I64, F64, P, I64, P, I64, F64, P, I64]),
     "ipm_transpose": (C.c_int, [P, I64, I64, P, I64, P, I64]),

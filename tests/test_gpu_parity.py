@@ -243,51 +243,6 @@ def test_concurrent_instances_match_sequential():
         np.testing.assert_array_equal(np.array(s.xstar), ref)
 
 
-def test_batch_group_matches_sequential():
-    """Config-4 batch group (ipm355.batch.BatchGroup): instances solved from host threads on their
-    own streams whose Newton-step Cholesky factorisations run as ONE grid give results bit-identical
-    to solving them one by one (each instance keeps its own tickets and tile order), and the group
-    actually batched (more member factorisations than leader launches)."""
-    import threading
-
-    import torch
-
-    import ipm355
-    from ipm355 import problems
-    from ipm355.batch import BatchGroup
-    kws = [dict(problems.qp_ineq_box(300, 80, seed=70 + i), **problems.QP_KWARGS) for i in range(6)]
-    seq = []
-    for kw in kws:
-        s = ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw)
-        s.solve()
-        seq.append((np.array(s.xstar), list(s.inner_iters)))
-    group = BatchGroup(timeout_us=2000)
-    streams = [torch.cuda.Stream() for _ in kws]
-    solvers = []
-    for kw, st in zip(kws, streams):
-        with torch.cuda.stream(st):
-            s = ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw)
-        group.attach(s)
-        solvers.append(s)
-
-    def run(k):
-        with torch.cuda.stream(streams[k]), group.member():
-            solvers[k].solve()
-    th = [threading.Thread(target=run, args=(k,)) for k in range(len(kws))]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    torch.cuda.synchronize()
-    launches, batched = group.stats()
-    print(f"batch group: {batched} factorisations in {launches} launches")
-    for s, (x, its) in zip(solvers, seq):
-        assert list(s.inner_iters) == its
-        np.testing.assert_array_equal(np.array(s.xstar), x)
-    assert batched > launches
-    group.close()
-
-
 @pytest.mark.parametrize("knobs", [
     {"IPM_DEFER_KS": "256"},
     {"IPM_DEFER_KS": "64"},
