@@ -10,7 +10,9 @@ OBJ_DIR  := build/obj
 # dot products and MFMA use explicit fma where intended.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-result -Wno-unused-value -Iinclude -I$(SRC_DIR)
-SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip $(SRC_DIR)/ipm_lasso.hip
+SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip $(SRC_DIR)/ipm_lasso.hip $(SRC_DIR)/ipm_lstsq.hip
+# rocSOLVER (dsyevd) + rocBLAS (dgemm): the least-squares fallback only (ipm_lstsq.hip)
+LIBS     := -L/opt/rocm/lib -lrocsolver -lrocblas -Wl,-rpath,/opt/rocm/lib
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
 HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
 
@@ -21,7 +23,7 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OUT): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ $(LIBS)
 
 # diagnostic library: per-workgroup role timestamps of one Cholesky launch (IPM_TRACE_BLOCK=b),
 # loaded with IPM355_LIB=build/trace/libipm355_trace.so (scripts/role_trace.py)
@@ -31,7 +33,7 @@ $(TRACE_OUT): $(SRCS) $(HDRS)
 	@mkdir -p build/trace
 	$(HIPCC) $(HIPFLAGS) -DIPM_ROLE_TRACE -c $(SRC_DIR)/ipm_blas.hip -o build/trace/ipm_blas.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC build/trace/ipm_blas.o $(OBJ_DIR)/ipm_barrier.o \
-	    $(OBJ_DIR)/ipm_engine.o $(OBJ_DIR)/ipm_lasso.o -o $@
+	    $(OBJ_DIR)/ipm_engine.o $(OBJ_DIR)/ipm_lasso.o $(OBJ_DIR)/ipm_lstsq.o -o $@ $(LIBS)
 
 clean:
 	rm -rf build $(OUT)

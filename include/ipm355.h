@@ -43,7 +43,10 @@ extern "C" {
 /* linear-solve strategies (dispatch tables LPSolver.py:371-469, QPSolver.py:385-455) */
 #define IPM_SOLVE_CHOLESKY 0 /* dense Cholesky; first failure -> permanent fallback (Q9) */
 #define IPM_SOLVE_DIAGONAL 1 /* H diagonal (LP, C is None, try_diag) */
-#define IPM_SOLVE_LU 2       /* np_solve: LU with partial pivoting */
+#define IPM_SOLVE_LU 2       /* np_solve / direct: LU with partial pivoting */
+#define IPM_SOLVE_LSTSQ 3    /* np_lstsq: minimum-norm least squares (lstsq(H, -g, rcond=None)) */
+#define IPM_SOLVE_DIAGONAL_LSTSQ 4 /* diagonal H, equality system S = A H^-1 A^T by lstsq
+                                      (NewtonSolverNPLstSqDiagonalInfeasibleStart) */
 
 typedef struct ipm_handle ipm_handle;
 typedef struct ipm_problem ipm_problem;
@@ -201,6 +204,13 @@ int ipm_getrf(ipm_handle* h, int64_t n, double* A, int64_t lda, int64_t* piv, in
 /* solve with the ipm_getrf factors; B row-major n x nrhs (ldb), in place */
 int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
               double* B, int64_t ldb);
+/* minimum-norm least squares on a symmetric matrix: B <- A^+ B, the np.linalg.lstsq(A, B, rcond=None)
+   of the np_lstsq method and of the Cholesky-failure backup (NewtonSolver.py:212-227, 334-341;
+   NewtonSolverInfeasibleStart.py:279-316, 692-724).  A full symmetric (column-major, lda), replaced
+   by its eigenvectors; eigenvalues |lambda| <= eps * n * max|lambda| are dropped (gelsd's rcond
+   rule).  B row-major n x nrhs (ldb), in place.  *info: the eigensolver's convergence info (0 = ok) */
+int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda, double* B, int64_t ldb,
+                  int* info);
 /* HIP-event timing of the KKT assembly and of the Cholesky factorisation inside
    ipm_newton_solve (enable/reset with ipm_set_timing; adds no synchronisation):
    averages (ms) over the Newton iterations since the reset, and their count */

@@ -147,6 +147,15 @@ void getrf(hipStream_t s, int64_t n, double* A, int64_t lda, int64_t* piv, int* 
 inline int64_t getrf_ws_doubles(int64_t n) { return 64 * (n + 1); }
 void getrs(hipStream_t s, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
            double* B, int64_t ldb);
+// minimum-norm least squares on a symmetric matrix, np.linalg.lstsq(H, B, rcond=None) (ipm_lstsq.hip):
+// factor = eigendecomposition (A full column-major -> eigenvectors in place, ws[0:n] the
+// pseudo-inverse weights), apply = B (row-major n x nrhs) <- H^+ B.  rb: lazily created library
+// handle slot.  ws: lstsq_ws_doubles(n, nrhs) doubles.  Return 0, or -1 on a library error.
+int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs);
+int lstsq_sym_factor(void** rb, hipStream_t s, int64_t n, double* A, int64_t lda, double* ws, int* info_dev);
+int lstsq_sym_apply(void** rb, hipStream_t s, int64_t n, int64_t nrhs, const double* V, int64_t ldv, double* B,
+                    int64_t ldb, double* ws);
+void lstsq_release(void* rb);
 
 // small helpers
 void fill(hipStream_t s, double* p, int64_t n, double v);

@@ -61,7 +61,7 @@ struct ipm_problem {
   // dims / flags
   int64_t n = 0, N = 0, S = 0, Sbar = 0, nub = 0, nlb = 0, m = 0, p = 0, K = 0, R = 0, XR = 0, Lh = 0;
   int64_t ldh = 0, nbb = 0;  // ld of H, bound-segment length (SOCP)
-  bool lp = false, qp = false, socp = false, ph1 = false, eq = false, diag = false, lu = false;
+  bool lp = false, qp = false, socp = false, ph1 = false, eq = false, diag = false, lu = false, lsq = false;
   SocpView sv{};
   // workspace carve
   double *xe = nullptr, *s0 = nullptr, *ds = nullptr, *inv = nullptr, *w = nullptr, *dvec = nullptr;
@@ -121,8 +121,9 @@ void derive(ipm_problem* pr) {
   pr->nlb = d.lb ? d.n : 0;
   pr->p = d.A ? d.p : 0;
   pr->eq = pr->p > 0;
-  pr->diag = d.solve_method == IPM_SOLVE_DIAGONAL;
+  pr->diag = d.solve_method == IPM_SOLVE_DIAGONAL || d.solve_method == IPM_SOLVE_DIAGONAL_LSTSQ;
   pr->lu = d.solve_method == IPM_SOLVE_LU;
+  pr->lsq = d.solve_method == IPM_SOLVE_LSTSQ || d.solve_method == IPM_SOLVE_DIAGONAL_LSTSQ;
   if (pr->socp) {
     pr->K = d.K;
     pr->R = d.R;
@@ -477,6 +478,7 @@ extern "C" int ipm_destroy(ipm_handle* h) {
   if (h->dinfo) hipFree(h->dinfo);
   if (h->pws) hipFree(h->pws);
   if (h->scratch) hipFree(h->scratch);
+  lstsq_release(h->rb);
   for (auto& ev : h->ev) hipEventDestroy(ev);
   for (hipEvent_t e : {h->pst.ev_rel, h->pst.ev_pan, h->pst.ev_in, h->pst.ev_out})
     if (e) hipEventDestroy(e);
@@ -576,6 +578,27 @@ extern "C" int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L
   return IPM_OK;
 }
 
+extern "C" int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda, double* B, int64_t ldb,
+                             int* info) {
+  if (!h || n < 0 || nrhs < 0 || lda < n || ldb < nrhs) return IPM_INVALID_ARG;
+  if (info) *info = 0;
+  if (n == 0 || nrhs == 0) return IPM_OK;
+  double* lw = scratch(h, (size_t)lstsq_ws_doubles(n, nrhs) * sizeof(double));
+  if (!lw) { h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  if (lstsq_sym_factor(&h->rb, h->stream, n, A, lda, lw, h->dinfo) ||
+      lstsq_sym_apply(&h->rb, h->stream, n, nrhs, A, lda, B, ldb, lw)) {
+    h->err = "least-squares library call failed";
+    return IPM_HIP_ERROR;
+  }
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int inf;
+  std::memcpy(&inf, h->hbuf, sizeof(int));
+  if (info) *info = inf;
+  return IPM_OK;
+}
+
 extern "C" int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count) {
   // averages over the Newton iterations since ipm_set_timing(h, 1)
   if (!h) return IPM_INVALID_ARG;
@@ -651,7 +674,7 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
     return IPM_INVALID_ARG;
   }
   carve(pr, reinterpret_cast<char*>(workspace));
-  pr->use_backup = d.solve_method == IPM_SOLVE_LU;
+  pr->use_backup = d.solve_method == IPM_SOLVE_LU || d.solve_method == IPM_SOLVE_LSTSQ;
   if (!pr->defer_d.empty() && (d.ldc & 1) == 0 && (((uintptr_t)d.C) & 15) == 0) {
     // deferred KKT slices: the up-front K extent per block, uploaded once
     DeferSyrk& ds = pr->dsy;
@@ -955,7 +978,22 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
     if (h->timing) hipEventRecord(h->ev[3], st);
     trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv);
+  } else if (!pr->lu) {
+    // np_lstsq, and the Cholesky-failure backup (NewtonSolver.py:212-227, 334-341):
+    // lstsq(H, -g, rcond=None), minimum norm on the eigenvectors of H
+    lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
+    int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
+    if (rc) return rc;
+    double* lw = scratch(pr->h, (size_t)lstsq_ws_doubles(pr->N, 1) * sizeof(double));
+    if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+    if (lstsq_sym_factor(&pr->h->rb, st, pr->N, pr->H, pr->ldh, lw, pr->info) ||
+        lstsq_sym_apply(&pr->h->rb, st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, lw)) {
+      pr->h->err = "least-squares library call failed";
+      return IPM_HIP_ERROR;
+    }
+    hipMemsetAsync(pr->info, 0, sizeof(int), st);
   } else {
+    // np_solve / direct: LU with partial pivoting (NewtonSolver.py:230-247, 344-361)
     lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
     if (rc) return rc;
@@ -965,6 +1003,47 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     getrs(st, pr->N, 1, pr->H, pr->ldh, pr->piv, pr->dx, 1);
     hipMemsetAsync(pr->info, 0, sizeof(int), st);
   }
+  return IPM_OK;
+}
+
+// np_lstsq block elimination (NewtonSolverInfeasibleStart.py:279-316): four lstsq calls, three of
+// them on A11 = H (one eigendecomposition shared), one on S = A H^+ A^T.  Expects H assembled and
+// pr->Axb = A x - b; writes dx, dv.
+int direction_infeasible_lstsq(ipm_problem* pr, const double* v) {
+  const ipm_problem_desc& d = pr->d;
+  hipStream_t st = S(pr);
+  const int64_t n = pr->n, p = pr->p, lds = p + (p & 1);
+  int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
+  if (rc) return rc;
+  // one scratch carve (the handle scratch is shared: expand_full_inplace would reuse its start)
+  const int64_t wh = lstsq_ws_doubles(n, p), ws = lstsq_ws_doubles(p, 1);
+  double* lw = scratch(pr->h, (size_t)(wh + ws + std::max<int64_t>(p * lds, 1)) * sizeof(double));
+  if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  double* lws = lw + wh;
+  double* stmp = lws + ws;
+  void** rb = &pr->h->rb;
+  bool bad = lstsq_sym_factor(rb, st, n, pr->H, pr->ldh, lw, pr->info) != 0;
+  // Y = H^+ A^T (n x p row-major), hg = H^+ g
+  copy(st, pr->Ybuf, d.AT, n * p);
+  bad = bad || lstsq_sym_apply(rb, st, n, p, pr->H, pr->ldh, pr->Ybuf, p, lw) != 0;
+  copy(st, pr->tmpn, pr->g, n);
+  bad = bad || lstsq_sym_apply(rb, st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, lw) != 0;
+  // S = A Y, w = S^+ (b2 - A hg)
+  SyrkEpi e;
+  syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
+  sym_lower_to_full(st, p, pr->Sbuf, lds, stmp, lds);
+  copy(st, pr->Sbuf, stmp, p * lds);
+  bad = bad || lstsq_sym_factor(rb, st, p, pr->Sbuf, lds, lws, pr->info + 1) != 0;
+  gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
+  lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
+  bad = bad || lstsq_sym_apply(rb, st, p, 1, pr->Sbuf, lds, pr->wv, 1, lws) != 0;
+  // dx = -H^+ (g + A^T w)
+  gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
+  lincomb(st, n, -1.0, pr->g, -1.0, pr->ATdv, pr->dx);
+  bad = bad || lstsq_sym_apply(rb, st, n, 1, pr->H, pr->ldh, pr->dx, 1, lw) != 0;
+  if (bad) { pr->h->err = "least-squares library call failed"; return IPM_HIP_ERROR; }
+  lincomb(st, p, 1.0, pr->wv, -1.0, v, pr->dv);
+  hipMemsetAsync(pr->info, 0, 2 * sizeof(int), st);
   return IPM_OK;
 }
 
@@ -986,12 +1065,33 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     const int64_t lds = p + (p & 1);
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, nullptr, 0, pr->tmpn, 0.0, pr->Sbuf, lds, e);
-    potrf_lower(st, p, pr->Sbuf, lds, pr->info, pr->pws);
+    double* lw = nullptr;
+    if (pr->lsq) {
+      // NewtonSolverNPLstSqDiagonalInfeasibleStart (NewtonSolverInfeasibleStart.py:692-724): w = lstsq(S, r)
+      int rc = expand_full_inplace(pr, pr->Sbuf, p, lds);
+      if (rc) return rc;
+      lw = scratch(pr->h, (size_t)lstsq_ws_doubles(p, 1) * sizeof(double));
+      if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+      if (lstsq_sym_factor(&pr->h->rb, st, p, pr->Sbuf, lds, lw, pr->info)) {
+        pr->h->err = "least-squares library call failed";
+        return IPM_HIP_ERROR;
+      }
+    } else {
+      potrf_lower(st, p, pr->Sbuf, lds, pr->info, pr->pws);
+    }
     // r = b2 - A (Hi * g)
     mul(st, n, pr->tmpn, pr->g, 1.0, pr->hxs);
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->hxs, 0.0, pr->r2);
     lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
-    potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp, pr->ctl);
+    if (pr->lsq) {
+      if (lstsq_sym_apply(&pr->h->rb, st, p, 1, pr->Sbuf, lds, pr->wv, 1, lw)) {
+        pr->h->err = "least-squares library call failed";
+        return IPM_HIP_ERROR;
+      }
+      hipMemsetAsync(pr->info, 0, sizeof(int), st);
+    } else {
+      potrs_lower(st, p, 1, pr->Sbuf, lds, pr->wv, 1, pr->Wp, pr->ctl);
+    }
     // dx = (-Hi) * (g + A^T w)
     gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
     lincomb(st, n, 1.0, pr->g, 1.0, pr->ATdv, pr->hxs);
@@ -1030,6 +1130,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     lincomb(st, p, 1.0, pr->wv, -1.0, v, pr->dv);
     return IPM_OK;
   }
+  if (pr->lsq) return direction_infeasible_lstsq(pr, v);
   // LU fallback: four np.linalg.solve (NewtonSolverInfeasibleStart.py:513-538)
   int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
   if (rc) return rc;

@@ -22,6 +22,7 @@ struct ipm_handle {
   int64_t pws_n = 0;
   double* scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* rb = nullptr;      // library handle for the least-squares fallback (ipm_lstsq.hip), lazy
   hipEvent_t ev[6];
   double kkt_sum = 0.0, potrf_sum = 0.0;
   int64_t kkt_cnt = 0, potrf_cnt = 0;

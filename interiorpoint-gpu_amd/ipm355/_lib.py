@@ -20,7 +20,7 @@ IPM_INVALID_ARG = 2
 IPM_HIP_ERROR = 3
 
 KIND_LP, KIND_QP, KIND_SOCP = 0, 1, 2
-SOLVE_CHOLESKY, SOLVE_DIAGONAL, SOLVE_LU = 0, 1, 2
+SOLVE_CHOLESKY, SOLVE_DIAGONAL, SOLVE_LU, SOLVE_LSTSQ, SOLVE_DIAGONAL_LSTSQ = 0, 1, 2, 3, 4
 LS_TABLE, LS_EXACT, LS_COMPARE = 0, 1, 2
 
 P = C.c_void_p
@@ -86,6 +86,7 @@ EXPORTS = {
     "ipm_potrs": (C.c_int, [P, I64, I64, P, I64, P, I64]),
     "ipm_getrf": (C.c_int, [P, I64, P, I64, P, C.POINTER(C.c_int)]),
     "ipm_getrs": (C.c_int, [P, I64, I64, P, I64, P, P, I64]),
+    "ipm_lstsq_sym": (C.c_int, [P, I64, I64, P, I64, P, I64, C.POINTER(C.c_int)]),
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),

@@ -44,7 +44,7 @@ class NewtonSolver:
         self.phase1_flag, self.phase1_tol = phase1_flag, phase1_tol
         self.use_psd_condition = use_psd_condition
         self.update_slacks_every = update_slacks_every
-        if self.method == "lu" and self.fm is not None:
+        if self.method in ("lu", "lstsq") and self.fm is not None:
             self.fm.prob.use_backup = True       # np.linalg.solve / lstsq / inv from the start
         self.last_result = None
         self.trace = []          # per-iteration (step, nd | residual) like the oracle's trace
@@ -84,7 +84,8 @@ class NewtonSolver:
 
 
 class NewtonSolverCholesky(NewtonSolver):
-    """NewtonSolver.py:250-341: Cholesky; first failure -> permanent fallback (Q9)."""
+    """NewtonSolver.py:250-341: Cholesky; first failure -> permanent fallback (Q9): from then on
+    lstsq(H, -g, rcond=None) (backup_solve, :334-341), the device minimum-norm solve."""
 
 
 class NewtonSolverDiagonal(NewtonSolver):
@@ -97,9 +98,10 @@ class NewtonSolverNPSolve(NewtonSolver):
     method = "lu"
 
 
-class NewtonSolverNPLstSq(NewtonSolverNPSolve):
-    """NewtonSolver.py:212-227: lstsq.  On the device this is the LU solve, identical for
-    nonsingular H; exactly-zero pivot columns get a zero component (min-norm for those)."""
+class NewtonSolverNPLstSq(NewtonSolver):
+    """NewtonSolver.py:212-227: lstsq(H, -g, rcond=None) -> the device minimum-norm solve
+    (eigenvectors of H, |lambda| <= eps n max|lambda| dropped: gelsd's rcond rule)."""
+    method = "lstsq"
 
 
 class NewtonSolverDirect(NewtonSolverNPSolve):
@@ -136,8 +138,9 @@ class NewtonSolverNPSolveInfeasibleStart(NewtonSolverInfeasibleStart):
     method = "lu"
 
 
-class NewtonSolverNPLstSqInfeasibleStart(NewtonSolverNPSolveInfeasibleStart):
-    pass
+class NewtonSolverNPLstSqInfeasibleStart(NewtonSolverInfeasibleStart):
+    """NewtonSolverInfeasibleStart.py:279-316: block elimination with four lstsq calls."""
+    method = "lstsq"
 
 
 class NewtonSolverDirectInfeasibleStart(NewtonSolverNPSolveInfeasibleStart):
@@ -171,6 +174,10 @@ class NewtonSolverNPSolveDiagonalInfeasibleStart(NewtonSolverCholeskyDiagonalInf
     """Diagonal H: S = A diag(1/h) A^T solved by Cholesky on the device (same system)."""
 
 
-NewtonSolverNPLstSqDiagonalInfeasibleStart = NewtonSolverNPSolveDiagonalInfeasibleStart
+class NewtonSolverNPLstSqDiagonalInfeasibleStart(NewtonSolverCholeskyDiagonalInfeasibleStart):
+    """NewtonSolverInfeasibleStart.py:692-724: diagonal H, w = lstsq(A diag(1/h) A^T, r)."""
+    method = "diag_lstsq"
+
+
 NewtonSolverDirectDiagonalInfeasibleStart = NewtonSolverNPSolveDiagonalInfeasibleStart
 NewtonSolverKKTNPSolveDiagonalInfeasibleStart = NewtonSolverNPSolveDiagonalInfeasibleStart

@@ -89,8 +89,12 @@ def _infeasible_class(method, diag):
 def _solve_method_for(cls):
     if cls.method == "diag":
         return L.SOLVE_DIAGONAL
+    if cls.method == "diag_lstsq":
+        return L.SOLVE_DIAGONAL_LSTSQ
     if cls.method == "lu":
         return L.SOLVE_LU
+    if cls.method == "lstsq":
+        return L.SOLVE_LSTSQ
     return L.SOLVE_CHOLESKY
 
 
@@ -308,7 +312,7 @@ class LPSolver(_BarrierSolver):
             cls = _feasible_class(linear_solve_method, diag)
             if cls is None:
                 raise ValueError("No KKT System non-equality-constrained problems! Please choose another solver")
-        if cls.method == "diag" and C is None and not self.bounded:
+        if cls.method in ("diag", "diag_lstsq") and C is None and not self.bounded:
             cls = NS.NewtonSolverCholesky if not self.equality_constrained else NS.NewtonSolverCholeskyInfeasibleStart
         self.fm = FunctionManagerLP(c=c, A=A, b=b, C=C, d=d, x0=self.x, lower_bound=self.lb, upper_bound=self.ub,
                                     t=1, n=self.n, try_diag=try_diag, solve_method=_solve_method_for(cls),

@@ -372,6 +372,22 @@ def extra():
                                                           linear_solve_method=meth))
 
 
+def lstsq_singular():
+    """Rank-deficient Newton systems: an LP with more variables than inequality rows and no bounds,
+    so H = C^T diag(1/s^2) C has rank m < n at every step.  lstsq(H, -g, rcond=None) then returns
+    the minimum-norm step (NewtonSolver.py:212-227), and the Cholesky class fails at its first step
+    and continues on the same lstsq backup (Q9, NewtonSolver.py:314-341).  c = -C^T lam (lam > 0)
+    keeps the LP bounded on x0 + range(C^T), which is where minimum-norm steps keep the iterates."""
+    for (n, m, seed) in ((100, 30, 3), (64, 16, 4)):
+        rng = np.random.default_rng(seed)
+        C = np.round(rng.uniform(-2, 2, (m, n)) * 1024) / 1024
+        c = -C.T @ rng.uniform(0.5, 2, m)
+        d = np.round(rng.uniform(1, 3, m) * 1024) / 1024
+        for meth in ("np_lstsq", "cholesky"):
+            run_solve(f"lsq_sing_lp{n}_{meth}", RefLP, dict(c=c, C=C, d=d, lower_bound=None, upper_bound=None, x0=np.zeros(n),
+                                                            linear_solve_method=meth))
+
+
 if __name__ == "__main__":
     _wrap_feasible()
     if sys.argv[1:] == ["extra"]:
@@ -380,6 +396,8 @@ if __name__ == "__main__":
         eq_many()
     elif sys.argv[1:] == ["npy_lp"]:
         npy_lp()
+    elif sys.argv[1:] == ["lstsq_singular"]:
+        lstsq_singular()
     elif sys.argv[1:] == ["eq_box_stable"]:
         eq_box_stable()
     else:

@@ -22,6 +22,9 @@ SOLVE_CASES = {
 METHOD_CASES = {f"meth_{case}_{meth}": kind
                 for case, kind in (("qp_ineq_box", "QP"), ("qp_eq_phase1", "QP"), ("lp_ineq_box", "LP"))
                 for meth in ("np_solve", "np_lstsq", "direct")}
+# rank-deficient H (LP, n > m, no bounds): np_lstsq, and the Cholesky class on its lstsq backup
+# (make_golden.py lstsq_singular) -- minimum-norm steps, where an LU solve has no answer
+METHOD_CASES.update({f"lsq_sing_lp{n}_{meth}": "LP" for n in (100, 64) for meth in ("np_lstsq", "cholesky")})
 
 # kwargs that are stored as scalars in the fixture but are not array inputs
 _SCALAR_KW = {"t0", "mu", "epsilon", "alpha", "beta", "max_inner_iters", "max_outer_iters",

@@ -198,6 +198,42 @@ def test_getrf_getrs_match_numpy(n):
     np.testing.assert_allclose(Bd.cpu().numpy(), ref, rtol=1e-8, atol=1e-10 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("n,rank,nrhs,indef", [(50, 50, 1, False), (200, 120, 3, False), (300, 90, 1, True),
+                                               (1025, 700, 2, False)])
+def test_lstsq_sym_matches_numpy(n, rank, nrhs, indef):
+    """Minimum-norm least squares (ipm_lstsq_sym: eigenvectors, gelsd's rcond = eps*n cut) vs
+    np.linalg.lstsq(H, B, rcond=None) -- the np_lstsq method and the Cholesky-failure backup
+    (NewtonSolver.py:212-227, 334-341).  Rank-deficient H (PSD, or indefinite) is where it differs
+    from an LU solve; B row-major n x nrhs."""
+    import ctypes
+    import torch
+    from gpu_util import handle
+    from ipm355 import _lib as L
+    h = handle()
+    rng = np.random.default_rng(n + rank)
+    G = rng.normal(size=(rank, n))
+    D = rng.uniform(0.5, 3.0, rank) * (np.where(rng.random(rank) < 0.5, -1.0, 1.0) if indef else 1.0)
+    H = G.T @ (D[:, None] * G)
+    H = 0.5 * (H + H.T)
+    B = rng.normal(size=(n, nrhs))
+    ref = np.linalg.lstsq(H, B, rcond=None)[0]
+    Ad = torch.as_tensor(H.copy(), device="cuda")              # symmetric: either layout
+    Bd = torch.as_tensor(B.copy(), device="cuda")
+    info = ctypes.c_int(-1)
+    assert h.lib.ipm_lstsq_sym(h.ptr, n, nrhs, L.dptr(Ad), n, L.dptr(Bd), nrhs, ctypes.byref(info)) == 0
+    assert info.value == 0
+    X = Bd.cpu().numpy()
+    # same minimum-norm vector: the error is the conditioning of the kept part times eps
+    err = np.linalg.norm(X - ref) / np.linalg.norm(ref)
+    print(f"[lstsq n={n} rank={rank}] rel {err:.1e}")
+    assert err <= 1e-8, err
+    if rank < n:
+        # no component in the null space of H (an LU solve of a singular H has no such property)
+        _, V = np.linalg.eigh(H)
+        null = V[:, :n - rank] if not indef else V[:, np.argsort(np.abs(np.linalg.eigvalsh(H)))[:n - rank]]
+        assert np.linalg.norm(null.T @ X) <= 1e-8 * np.linalg.norm(X)
+
+
 @pytest.mark.parametrize("n,nrhs", [(130, 40), (1030, 300), (2100, 64), (4097, 4097)])
 def test_potrs_many_rhs_blocked(n, nrhs):
     """L L^T X = B with many right-hand sides (128-row blocks on MFMA GEMMs, the Lasso's Q = M^-1)

@@ -305,12 +305,13 @@ def test_other_linear_solve_methods(name, method):
     c = cls_cpu(**kw)
     vc = c.solve()
     err = rel(s.xstar, c.xstar)
-    if name == "lp_eq_ineq":
+    if name == "lp_eq_ineq" and method != "np_lstsq":
         # this trajectory passes through Newton steps where backtracking gets stuck on nearly
         # singular H (t ~ 1e7): there the LU direction is rounding noise of the LU algorithm
         # itself (LAPACK's blocked recursive dgetrf vs the device's right-looking one), so the
         # trajectories part; parity is required at the objective (1e-4 relative) and the x*
-        # divergence is reported, not asserted
+        # divergence is reported, not asserted.  np_lstsq drops those directions
+        # (minimum norm) on both sides and is held to the full bar below.
         print(f"[{name}/{method}] x* rel {err:.1e}, value {v:.10g} vs {vc:.10g}, iters "
               f"{list(s.inner_iters)} vs {list(c.inner_iters)}")
         assert abs(v - vc) <= 1e-4 * max(1.0, abs(vc))
@@ -332,6 +333,8 @@ def test_linear_solve_methods_vs_reference(name):
     print(f"[{name}] x* rel {err:.1e} (tol {xtol:.1e}), iters {list(s.inner_iters)} vs {list(z['inner_iters'])}")
     assert err <= xtol, err
     assert abs(v - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * max(1.0, abs(float(z["value"])))
+    if name.startswith("lsq_sing") and name.endswith("cholesky"):
+        assert s.ns.use_backup and bool(z["use_backup"])      # Q9 fired on the singular H
     if bool(z["sens_iters_stable"]):
         assert list(s.inner_iters) == list(z["inner_iters"])
         steps = [t[0] for t in ((s.phase1_solver.phase1_ns.trace if len(z["phase1_inner_iters"]) else [])
