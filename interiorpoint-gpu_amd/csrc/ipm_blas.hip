@@ -40,14 +40,34 @@ __global__ __launch_bounds__(256) void k_gemv_n(int64_t rows, int64_t cols, doub
   const double* mr = M + row * ldm;
   double acc0 = 0.0, acc1 = 0.0;
   if (VEC) {
+    // four 16-byte loads of the row in flight per lane (one per 64-lane stride), eight partial
+    // sums folded in a fixed order: the row streams at HBM rate instead of one load per trip
     const int64_t c2 = cols >> 1;
     const double2* m2 = reinterpret_cast<const double2*>(mr);
     const double2* x2 = reinterpret_cast<const double2*>(x);
-    for (int64_t j = lane; j < c2; j += 64) {
-      double2 a = m2[j], b = x2[j];
-      acc0 = fma(a.x, b.x, acc0);
-      acc1 = fma(a.y, b.y, acc1);
+    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int64_t j = lane;
+    for (; j + 192 < c2; j += 256) {
+      typedef double nt2 __attribute__((ext_vector_type(2)));
+      nt2 u[4];
+      double2 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = __builtin_nontemporal_load(reinterpret_cast<const nt2*>(m2 + j + 64 * q));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = x2[j + 64 * q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[2 * q] = fma(u[q].x, v[q].x, a[2 * q]);
+        a[2 * q + 1] = fma(u[q].y, v[q].y, a[2 * q + 1]);
+      }
     }
+    for (; j < c2; j += 64) {
+      const double2 u = m2[j], v = x2[j];
+      a[0] = fma(u.x, v.x, a[0]);
+      a[1] = fma(u.y, v.y, a[1]);
+    }
+    acc0 = (a[0] + a[2]) + (a[4] + a[6]);
+    acc1 = (a[1] + a[3]) + (a[5] + a[7]);
     if ((cols & 1) && lane == 0) acc0 = fma(mr[cols - 1], x[cols - 1], acc0);
   } else {
     for (int64_t j = lane; j < cols; j += 64) acc0 = fma(mr[j], x[j], acc0);
@@ -147,6 +167,7 @@ void gemv_t(hipStream_t st, int64_t rows, int64_t cols, double alpha, const doub
 //   H(i,j) = alpha * sum_k w[k] X[k][i] Y[k][j] + beta*H(i,j) + tP*P[j][i] + [i==j] dvec[i]
 //   for the lower triangle i >= j; H column-major (element (i,j) at j*ldh + i).
 // =====================================================================================
+static int num_cus();
 static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
                         const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
                         const SyrkEpi& e, const int* info) {
@@ -207,7 +228,8 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
       return;
     }
   }
-  mfma_gemm_launch(st, a);
+  if (e.split_ws) mfma_gemm_launch_split(st, a, e.split_ws, e.split_cap, 2 * num_cus());
+  else mfma_gemm_launch(st, a);
 }
 
 void syrk_lower(hipStream_t st, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
@@ -1329,6 +1351,8 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         const int64_t st = v - 1, u = st - b.s_full;
         const int sp = u < 0 ? 0 : ((u & 1) ? 2 : 1);
         const int64_t p = u < 0 ? 0 : (u >> 1);
+        // (the branch-free slab loop of the KKT SYRK is not used here: inside this kernel it raised
+        // the SGPR spills 89 -> 621 and the factorisation took 2.5 % longer)
         mfma_tile<128, false, VEC, 2, false>(b.s, u < 0 ? st : b.s_full + p, sm.g128, sp, b.sscr + p * (128 * 128),
                                              b.sflag + p);
       }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace ipm {
 
 constexpr int WAVE = 64;
@@ -51,7 +53,20 @@ struct SyrkEpi {
   const int* kend_dev = nullptr;
   const int* kend_host = nullptr;
   int nkend = 0;
+  // split tail (k_mfma_gemm_split): split_cap partial tiles of 128 x 128, then split_cap flags;
+  // null: the plain tile grid
+  double* split_ws = nullptr;
+  int64_t split_cap = 0;
 };
+// workspace of the split tail for an n x n lower-triangle SYRK: the cap and its size in doubles
+inline int64_t syrk_split_cap(int64_t n) {
+  const int64_t T = (n + 63) / 64;   // 64-tile grid (the launcher uses 64-tiles below 768 128-tiles)
+  return std::min<int64_t>(256, std::max<int64_t>(T * (T + 1) / 2, 8));
+}
+inline int64_t syrk_split_ws_doubles(int64_t n) {
+  const int64_t c = syrk_split_cap(n);
+  return c * 128 * 128 + (c + 1) / 2 + 1;
+}
 void syrk_lower(hipStream_t s, int64_t n, int64_t k, double alpha, const double* X, int64_t ldx,
                 const double* Y, int64_t ldy, const double* w, double beta, double* H, int64_t ldh,
                 const SyrkEpi& epi);

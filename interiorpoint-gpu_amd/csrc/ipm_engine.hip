@@ -90,6 +90,7 @@ struct ipm_problem {
   int64_t defer_pairs = 0;
   int* kend_d = nullptr;
   double* Gd = nullptr;
+  double* sws = nullptr;   // KKT SYRK split tail (syrk_split_ws_doubles)
   DeferSyrk dsy;
   bool defer_on = false;
 };
@@ -224,6 +225,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   if (pr->eq) pe = std::max(pe, gemv_t_ws_elems(p, n));
   pr->part_elems = pe;
   pr->part = c.take<double>(pe);
+  if (!pr->diag && (pr->m > 0 || pr->socp)) pr->sws = c.take<double>(syrk_split_ws_doubles(n));
   pr->rowcone_d = c.take<int64_t>(pr->R + 1);
   pr->dslot_d = c.take<int64_t>(pr->K + 1);
   if (!pr->defer_d.empty()) {
@@ -380,6 +382,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool
       e.kend_host = pr->kend_h.data();
       e.nkend = (int)pr->kend_h.size();
     }
+    if (!defer && pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
     syrk_lower(st, pr->n, pr->m, 1.0, d.C, d.ldc, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // border: hxs = -C^T inv_C^2 + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (+psd)
@@ -402,6 +405,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool
     if (d.Kd > 0) dvec_diag_cones(st, pr->n, d.Kd, d.Ad, d.dcone_id, pr->coef, pr->dvec);
     if (d.P && !pr->ph1) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     e.dvec = pr->dvec;
+    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
     syrk_lower(st, pr->n, pr->XR, 1.0, d.X, d.ldx, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // hxs = -sum_i G_i inv_i + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (barrier segment)
@@ -513,6 +517,11 @@ extern "C" int ipm_syrk(ipm_handle* h, int64_t n, int64_t k, const double* X, in
                         double alpha, double beta, double* H, int64_t ldh) {
   if (!h || n < 0 || k < 0 || ldh < n || (k > 0 && ldx < n)) return IPM_INVALID_ARG;
   SyrkEpi e;
+  // the KKT SYRK's split tail (handle scratch), as inside the Newton step
+  if (double* sw = scratch(h, (size_t)syrk_split_ws_doubles(n) * sizeof(double))) {
+    e.split_ws = sw;
+    e.split_cap = syrk_split_cap(n);
+  }
   syrk_lower(h->stream, n, k, alpha, X, ldx, nullptr, 0, w, beta, H, ldh, e);
   HIPCHK(h, hipGetLastError());
   return IPM_OK;

@@ -22,6 +22,11 @@
 // Measured (tools/gemm_lab.hip, MI355X): 57 TF/s lower-triangle n=8192 K=2048, 50 TF/s at K=256.
 #pragma once
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <queue>
+#include <tuple>
+#include <vector>
 
 #include "ipm_common.h"
 
@@ -98,7 +103,14 @@ struct alignas(16) MfSmem {
 // accumulators start at 0, the tile -X^T Y goes to the scratch tile `part` (sc1, 128 x 128
 // column-major), then *pflag = 1.  SPLIT 2: k in [0, K/2) from the C tile as usual; before its
 // stores it waits for *pflag and adds `part`.  Only ever waits on a lower ticket.
-template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false>
+// SPLITADD: the non-accumulating epilogue (alpha acc + beta C + tP P + dvec) also takes the
+// upper-K partial of a split tile (the KKT SYRK's split tail, k_mfma_gemm_split); a separate
+// instantiation, so the Cholesky's tiles are compiled exactly as without it.
+// LOOP 1: the branch-free slab loop only -- the caller guarantees a full 128-tile, whole K slabs
+// (tile_fast_ok) and 16-byte operands; LOOP 0: the general loop only.  (Both loops in one
+// instantiation made the register allocator spill ~2000 VGPRs.)
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false, bool SPLITADD = false,
+          int LOOP = 0>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
                                           double* part = nullptr, unsigned* pflag = nullptr) {
   using M = MfCfg<BM_, WJ>;
@@ -152,7 +164,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     const double* xs = xp + s * xstep;
     const double* ys = yp + s * ystep;
     if (full && (s + 1) * BK <= Kt) {
-      const double wk = WEIGHT ? a.w[k] : 1.0;
+      const double wk = WEIGHT ? a.w[kbeg + k] : 1.0;   // k counts from this piece's first row
       if (VEC) {
 #pragma unroll
         for (int q = 0; q < PT / 2; ++q) {
@@ -172,7 +184,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
       }
     } else {
       const bool kin = k < Kt;
-      const double wk = (WEIGHT && kin) ? a.w[k] : 1.0;
+      const double wk = (WEIGHT && kin) ? a.w[kbeg + k] : 1.0;
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
         const bool xi = kin && (I0 + sc + q < a.ni), yj = kin && (J0 + sc + q < a.nj);
@@ -209,34 +221,92 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
         }
       }
   }
-  if (nslab > 0) {
-    gload(0);
-    sstore(0);
-    if (nslab > 1) gload(1);
-  }
-  __syncthreads();
-  for (int64_t s = 0; s < nslab; ++s) {
-    const int buf = (int)(s & 1);
-    const double* bx = sX[buf];
-    const double* by = sY[buf];
+  // full 128-tiles with whole K slabs: a branch-free slab loop -- ONE basic block, so the
+  // scheduler spreads the LDS reads, the LDS stores of slab s+1 and the global loads of slab s+2
+  // between the MFMAs (the last loads are clamped to slab nslab-1: a harmless reload).  The weight
+  // and the sign are applied when the slab goes to LDS.  tools/gemm_lab.hip (lab2): +6-9 %.
+  static_assert(LOOP == 0 || (BM_ == 128 && VEC && WJ == 2), "fast loop: 128-tiles, vector loads");
+  if (LOOP == 1) {
+    double fx[PT], fy[PT];
+    double fw = 1.0;
+    auto fload = [&](int64_t s) {
+      const double2* xs = reinterpret_cast<const double2*>(xp + s * xstep);
+      const double2* ys = reinterpret_cast<const double2*>(yp + s * ystep);
 #pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
-      double av[TWJ], bv[TWI];
+      for (int q = 0; q < PT / 2; ++q) {
+        const double2 u = xs[q], v = ys[q];
+        fx[2 * q] = u.x;
+        fx[2 * q + 1] = u.y;
+        fy[2 * q] = v.x;
+        fy[2 * q + 1] = v.y;
+      }
+      if (WEIGHT) fw = a.w[kbeg + s * BK + sr];
+    };
+    auto fstore = [&](int buf) {
 #pragma unroll
-      for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
+      for (int q = 0; q < PT; ++q) {
+        sX[buf][sr * LD + sc + q] = (WEIGHT ? fx[q] * fw : fx[q]) * xsg;
+        sY[buf][sr * LD + sc + q] = fy[q];
+      }
+    };
+    fload(0);
+    fstore(0);
+    fload(nslab > 1 ? 1 : 0);
+    __syncthreads();
+    for (int64_t s = 0; s < nslab; ++s) {
+      const int buf = (int)(s & 1);
+      const double* bx = sX[buf];
+      const double* by = sY[buf];
+      // slab s+1 to LDS (loaded during the previous slab; its buffer was last read before the
+      // barrier) and the loads of slab s+2 issued at once: they fly under all 64 MFMAs
+      fstore(buf ^ 1);
+      fload(std::min<int64_t>(s + 2, nslab - 1));
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < TWI; ++t) bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double av[TWJ], bv[TWI];
 #pragma unroll
-      for (int tj = 0; tj < TWJ; ++tj)
+        for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
 #pragma unroll
-        for (int ti = 0; ti < TWI; ++ti)
-          acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+        for (int t = 0; t < TWI; ++t) bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+      __syncthreads();
     }
-    if (s + 1 < nslab) {
-      sstore(buf ^ 1);
-      if (s + 2 < nslab) gload(s + 2);
+  } else {
+    if (nslab > 0) {
+      gload(0);
+      sstore(0);
+      if (nslab > 1) gload(1);
     }
     __syncthreads();
+    for (int64_t s = 0; s < nslab; ++s) {
+      const int buf = (int)(s & 1);
+      const double* bx = sX[buf];
+      const double* by = sY[buf];
+  #pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double av[TWJ], bv[TWI];
+  #pragma unroll
+        for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
+  #pragma unroll
+        for (int t = 0; t < TWI; ++t) bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
+  #pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+  #pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+      if (s + 1 < nslab) {
+        sstore(buf ^ 1);
+        if (s + 2 < nslab) gload(s + 2);
+      }
+      __syncthreads();
+    }
   }
   // ---- epilogue: lane holds D[j = fk + 4r][i = fr] of each 16 x 16 tile (f64 MFMA map,
   //      cdna_hip_programming.md §3) -> 16 consecutive lanes store 16 consecutive i
@@ -263,7 +333,9 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
             if (SC1OUT) st_sc1(cp, v);
             else *cp = v;
           } else {
-            double v = a.alpha * acc[tj][ti][r];
+            double av = acc[tj][ti][r];
+            if (SPLITADD && SPLIT == 2) av += ld_sc1(&part[(j - J0) * BM + (i - I0)]);
+            double v = a.alpha * av;
             if (a.beta != 0.0) v += a.beta * (*cp);
             if (a.P) v += a.tP * a.P[j * a.ldp + i];
             if (a.dvec && i == j) v += a.dvec[i];
@@ -277,6 +349,29 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     __syncthreads();
     if (tid == 0) __hip_atomic_store(pflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// the tile mfma_tile would take for index Lw (same enumeration), and whether it is full with whole
+// 16-row K slabs (no kend / split pieces: callers of the fast loop)
+template <int BM>
+__device__ __forceinline__ bool tile_fast_ok(const GemmArgs& a, int64_t Lw) {
+  int64_t L = Lw, bi, bj;
+  const int64_t q = a.nblk >> 3;
+  if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);
+  if (a.rowmajor) {
+    bi = L / a.tiles_j;
+    bj = L % a.tiles_j;
+  } else if (a.tri) {
+    int64_t b = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= L) ++b;
+    while (b * (b + 1) / 2 > L) --b;
+    bi = b;
+    bj = L - b * (b + 1) / 2;
+  } else {
+    bi = L % a.tiles_i;
+    bj = L / a.tiles_i;
+  }
+  return (bi + 1) * BM <= a.ni && (bj + 1) * BM <= a.nj && (a.K % 16) == 0 && a.kend256 == nullptr;
 }
 
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
@@ -295,7 +390,75 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
     if (s0 + l < s1) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, s0 + l, sm);
     return;
   }
-  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
+  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
+    if (BM_ == 128 && VEC && WJ == 2 && tile_fast_ok<BM_>(a, Lw))
+      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, false, (BM_ == 128 && VEC && WJ == 2) ? 1 : 0>(a, Lw, sm);
+    else
+      mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
+  }
+}
+
+// Split tail (the KKT SYRK): blocks [0, s_full) run whole tiles; then each of the last q tiles of
+// the enumeration as two K halves, the upper half first (lower blockIdx; blocks are dispatched in
+// order, so the half that waits always has its partner resident or done) -> partial tile in
+// sscr + p * BM * BM, flag sflag[p] (zeroed before the launch).  The last round of a
+// lower-triangle grid (e.g. 2080 tiles on 512 slots: a fifth round of 32) then runs as half
+// tiles on twice the slots.  The sum order (lower half, + upper half) is fixed: deterministic.
+template <int BM_, bool WEIGHT, bool VEC>
+__global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t s_full, double* sscr,
+                                                            unsigned* sflag) {
+  if (a.info && *a.info != 0) return;
+  __shared__ MfSmem<BM_, 2> sm;
+  const int64_t b = blockIdx.x;
+  constexpr int FL = (BM_ == 128 && VEC) ? 1 : 0;
+  if (b < s_full) {
+    if (FL && tile_fast_ok<BM_>(a, b)) mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, b, sm);
+    else mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, b, sm);
+    return;
+  }
+  const int64_t u = b - s_full, p = u >> 1;
+  double* part = sscr + p * (int64_t)(BM_ * BM_);
+  if (FL && (a.K % 32) == 0 && tile_fast_ok<BM_>(a, s_full + p))
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, s_full + p, sm, (u & 1) ? 2 : 1, part, sflag + p);
+  else
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, s_full + p, sm, (u & 1) ? 2 : 1, part, sflag + p);
+}
+
+// how many of nt tiles to split: list schedule on `slots` workgroup slots (2 per CU), whole tile
+// 1.0, half tile 0.55; the q with the smallest makespan (cached per grid)
+inline int64_t gemm_split_plan(int64_t nt, int slots, int64_t cap) {
+  if (nt <= 0 || slots <= 0) return 0;
+  static std::mutex mu;
+  static std::map<std::tuple<int64_t, int, int64_t>, int64_t> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_tuple(nt, slots, cap);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  auto mk = [&](int64_t q) {
+    std::priority_queue<double, std::vector<double>, std::greater<double>> pq;
+    for (int i = 0; i < slots; ++i) pq.push(0.0);
+    double m = 0.0;
+    auto put = [&](double d) {
+      const double t = pq.top() + d;
+      pq.pop();
+      pq.push(t);
+      m = std::max(m, t);
+    };
+    for (int64_t i = 0; i < nt - q; ++i) put(1.0);
+    for (int64_t i = 0; i < 2 * q; ++i) put(0.55);
+    return m;
+  };
+  double best = mk(0);
+  int64_t bq = 0;
+  for (int64_t q = 8; q <= std::min(nt, cap); q += 8) {
+    const double m = mk(q);
+    if (m < best - 0.02) {
+      best = m;
+      bq = q;
+    }
+  }
+  cache[key] = bq;
+  return bq;
 }
 
 template <int BM>
@@ -337,6 +500,43 @@ inline void mfma_gemm_launch(hipStream_t st, GemmArgs a) {
   const int64_t nblk128 = a.tri ? ti * (ti + 1) / 2 : ti * tj;
   if (nblk128 >= 768) mfma_gemm_launch_bm<128>(st, a, vec);
   else mfma_gemm_launch_bm<64>(st, a, vec);
+}
+
+// the KKT SYRK with its tail split (ws: cap * BM * BM doubles of partial tiles, then cap flags);
+// falls back to the plain launch when nothing is worth splitting
+inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64_t cap, int slots) {
+  if (a.ni <= 0 || a.nj <= 0) return;
+  const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
+                   ((((uintptr_t)a.Y) & 15) == 0);
+  const int64_t ti128 = (a.ni + 127) / 128, tj128 = (a.nj + 127) / 128;
+  const int64_t nblk128 = a.tri ? ti128 * (ti128 + 1) / 2 : ti128 * tj128;
+  const int BM = nblk128 >= 768 ? 128 : 64;
+  const int64_t ti = (a.ni + BM - 1) / BM, tj = (a.nj + BM - 1) / BM;
+  a.tiles_i = ti;
+  a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
+  const int64_t q = ws ? gemm_split_plan(a.nblk, slots, cap) : 0;
+  if (q == 0) {
+    if (BM == 128) mfma_gemm_launch_bm<128>(st, a, vec);
+    else mfma_gemm_launch_bm<64>(st, a, vec);
+    return;
+  }
+  const int64_t s_full = a.nblk - q;
+  unsigned* flags = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
+  hipMemsetAsync(flags, 0, q * sizeof(unsigned), st);
+  dim3 g((unsigned)(s_full + 2 * q)), b(256);
+#define IPM_SPLIT_LAUNCH(BMv)                                                                             \
+  do {                                                                                                    \
+    if (a.w) {                                                                                            \
+      if (vec) hipLaunchKernelGGL((k_mfma_gemm_split<BMv, true, true>), g, b, 0, st, a, s_full, ws, flags);   \
+      else hipLaunchKernelGGL((k_mfma_gemm_split<BMv, true, false>), g, b, 0, st, a, s_full, ws, flags);      \
+    } else {                                                                                              \
+      if (vec) hipLaunchKernelGGL((k_mfma_gemm_split<BMv, false, true>), g, b, 0, st, a, s_full, ws, flags);  \
+      else hipLaunchKernelGGL((k_mfma_gemm_split<BMv, false, false>), g, b, 0, st, a, s_full, ws, flags);     \
+    }                                                                                                     \
+  } while (0)
+  if (BM == 128) IPM_SPLIT_LAUNCH(128);
+  else IPM_SPLIT_LAUNCH(64);
+#undef IPM_SPLIT_LAUNCH
 }
 
 }  // namespace ipm

@@ -11,8 +11,11 @@ pytestmark = pytest.mark.gpu
 EPS = np.finfo(np.float64).eps
 
 
-@pytest.mark.parametrize("k,n", [(4, 16), (1, 1), (16, 128), (37, 130), (300, 257), (512, 1024), (0, 5)])
+@pytest.mark.parametrize("k,n", [(4, 16), (1, 1), (16, 128), (37, 130), (300, 257), (512, 1024), (0, 5),
+                                 (2050, 700), (64, 1000), (2048, 8192)])
 def test_syrk_weighted_matches_numpy(k, n):
+    """Includes grids whose tail runs as split K halves (k_mfma_gemm_split: n = 1000 and 1024 on
+    64-tiles -- every tile split, ragged edge tiles included -- and 8192 on 128-tiles)."""
     rng = np.random.default_rng(k * 1000 + n)
     X = rng.uniform(-2, 2, (k, n))
     w = rng.uniform(0.1, 3, k)

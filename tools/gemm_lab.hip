@@ -105,6 +105,197 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm(int n, int K, const doubl
   }
 }
 
+// k_gemm with a branch-free slab loop (one basic block: the slab s+2 loads are issued with the
+// slab index clamped, the LDS store of slab s+1 always happens) so that the scheduler can spread
+// the LDS reads, the LDS stores and the global loads between the MFMAs; SGB = 1 also pins an
+// interleave pattern with sched_group_barrier (mask 0x008 MFMA, 0x100 DS read, 0x200 DS write,
+// 0x020 VMEM read, 0x002 VALU)
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+__global__ __launch_bounds__(WM * WN * 64) void k_gemm2(int n, int K, const double* __restrict__ X, int ldx,
+                                                        const double* __restrict__ Y, int ldy,
+                                                        double* __restrict__ C, int ldc, int tiles_i, int nblk) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int LX = BM + 16, LY = BN + 16;
+  constexpr int PX = BK * BM / NT, PY = BK * BN / NT;
+  __shared__ double sX[2][BK * LX];
+  __shared__ double sY[2][BK * LY];
+  for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
+  int bi, bj;
+  if (TRI) {
+    const int L = Lp;
+    int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= L) ++b;
+    while (b * (b + 1) / 2 > L) --b;
+    bi = b; bj = L - b * (b + 1) / 2;
+  } else {
+    bi = Lp % tiles_i; bj = Lp / tiles_i;
+  }
+  const int I0 = bi * BM, J0 = bj * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv % WM, wj = wv / WM;
+  dbl4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = dbl4{0, 0, 0, 0};
+  constexpr int TPRX = BM / PX, TPRY = BN / PY;
+  const int xr = tid / TPRX, xc = (tid % TPRX) * PX;
+  const int yr = tid / TPRY, yc = (tid % TPRY) * PY;
+  double rx[PX], ry[PY];
+  const double* xb = X + (size_t)xr * ldx + I0 + xc;
+  const double* yb = Y + (size_t)yr * ldy + J0 + yc;
+  auto gload = [&](int s) {
+    const double2* xp = reinterpret_cast<const double2*>(xb + (size_t)s * BK * ldx);
+    const double2* yp = reinterpret_cast<const double2*>(yb + (size_t)s * BK * ldy);
+#pragma unroll
+    for (int q = 0; q < PX / 2; ++q) { double2 v = xp[q]; rx[2 * q] = v.x; rx[2 * q + 1] = v.y; }
+#pragma unroll
+    for (int q = 0; q < PY / 2; ++q) { double2 v = yp[q]; ry[2 * q] = v.x; ry[2 * q + 1] = v.y; }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < PX; ++q) sX[buf][xr * LX + xc + q] = rx[q];
+#pragma unroll
+    for (int q = 0; q < PY; ++q) sY[buf][yr * LY + yc + q] = ry[q];
+  };
+  const int nslab = K / BK;
+  gload(0); sstore(0);
+  gload(nslab > 1 ? 1 : 0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nslab; ++s) {
+    const int buf = s & 1;
+    const double* bx = sX[buf];
+    const double* by = sY[buf];
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[TN], b[TM];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) a[t] = by[(kk * 4 + fk) * LY + wj * (BN / WN) + t * 16 + fr];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) b[t] = bx[(kk * 4 + fk) * LX + wi * (BM / WM) + t * 16 + fr];
+#pragma unroll
+      for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TM; ++ti) acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tj], b[ti], acc[tj][ti], 0, 0, 0);
+    }
+    sstore(buf ^ 1);                          // slab s+1 (unused after the last slab)
+    gload(min(s + 2, nslab - 1));             // slab s+2 (clamped: a harmless reload at the end)
+    if (SGB == 1) {
+      // per k-step: its LDS reads first, then MFMAs with the stores / loads of the next slabs spread
+      constexpr int NM = TN * TM * (BK / 4), NR = (TN + TM) / 2 * (BK / 4);
+      constexpr int NW = (PX + PY) / 2, NG = (PX + PY) / 2;
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        else if (i - NR < NW) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        else if (i - NR - NW < NG) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+    for (int ti = 0; ti < TM; ++ti) {
+      const int i = I0 + wi * (BM / WM) + ti * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = J0 + wj * (BN / WN) + tj * 16 + fk + 4 * r;
+        if (!TRI || i >= j) C[(size_t)j * ldc + i] = acc[tj][ti][r];
+      }
+    }
+  __syncthreads();
+  }
+}
+
+// k_gemm2 with the slabs brought into LDS by the load itself (global_load_lds, 16 bytes per lane:
+// one wave instruction = one 128-double slab row): no register staging, no LDS store
+// instructions.  One slab of prefetch (the DMA of slab s+1 runs under slab s's MFMAs).
+template <int BM, int BN, int BK, bool TRI>
+__global__ __launch_bounds__(256, 2) void k_gemm3(int n, int K, const double* __restrict__ X, int ldx,
+                                                 const double* __restrict__ Y, int ldy,
+                                                 double* __restrict__ C, int ldc, int tiles_i, int nblk) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int LX = BM + 16, LY = BN + 16;
+  static_assert(BM == 128 && BN == 128, "one wave instruction per slab row");
+  __shared__ double sX[2][BK * LX];
+  __shared__ double sY[2][BK * LY];
+  for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
+  int bi, bj;
+  if (TRI) {
+    const int L = Lp;
+    int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= L) ++b;
+    while (b * (b + 1) / 2 > L) --b;
+    bi = b; bj = L - b * (b + 1) / 2;
+  } else {
+    bi = Lp % tiles_i; bj = Lp / tiles_i;
+  }
+  const int I0 = bi * BM, J0 = bj * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv % WM, wj = wv / WM;
+  dbl4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = dbl4{0, 0, 0, 0};
+  // wave wv loads slab rows wv, wv+4, wv+8, wv+12 of both operands: 8 instructions per slab
+  auto dma = [&](int s, int buf) {
+#pragma unroll
+    for (int r = 0; r < BK / 4; ++r) {
+      const int row = wv + 4 * r;
+      const double* gx = X + (size_t)(s * BK + row) * ldx + I0 + 2 * lane;
+      const double* gy = Y + (size_t)(s * BK + row) * ldy + J0 + 2 * lane;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gx,
+                                       (__attribute__((address_space(3))) void*)&sX[buf][row * LX], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gy,
+                                       (__attribute__((address_space(3))) void*)&sY[buf][row * LY], 16, 0, 0);
+    }
+  };
+  const int nslab = K / BK;
+  dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nslab; ++s) {
+    const int buf = s & 1;
+    dma(min(s + 1, nslab - 1), buf ^ 1);      // slab s+1 (a harmless reload after the last)
+    const double* bx = sX[buf];
+    const double* by = sY[buf];
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[TN], b[TM];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) a[t] = by[(kk * 4 + fk) * LY + wj * (BN / WN) + t * 16 + fr];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) b[t] = bx[(kk * 4 + fk) * LX + wi * (BM / WM) + t * 16 + fr];
+#pragma unroll
+      for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TM; ++ti) acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tj], b[ti], acc[tj][ti], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+    for (int ti = 0; ti < TM; ++ti) {
+      const int i = I0 + wi * (BM / WM) + ti * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = J0 + wj * (BN / WN) + tj * 16 + fk + 4 * r;
+        if (!TRI || i >= j) C[(size_t)j * ldc + i] = acc[tj][ti][r];
+      }
+    }
+  __syncthreads();
+  }
+}
+
 __global__ void k_ref(int n, int K, const double* X, int ldx, const double* Y, int ldy, double* C, int ldc) {
   int i = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
   if (i >= n) return;
@@ -119,6 +310,62 @@ void run(const char* name, int n, int K, double* X, double* Y, double* C, double
   const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
   auto launch = [&]() {
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, BK, TRI, PAD>), dim3(grid ? grid : nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti, nblk);
+  };
+  CK(hipMemset(C, 0, (size_t)n * n * 8));
+  launch();
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+  float best = 1e30, tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    hipEventRecord(a); launch(); hipEventRecord(b); hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b); best = std::min(best, ms); tot += ms;
+  }
+  // check a sample of columns
+  std::vector<double> hc((size_t)n * n), hr((size_t)n * n);
+  CK(hipMemcpy(hc.data(), C, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hr.data(), R, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  double err = 0, mx = 0;
+  for (int j = 0; j < n; j += 97)
+    for (int i = TRI ? j : 0; i < n; ++i) { err = std::max(err, fabs(hc[(size_t)j * n + i] - hr[(size_t)j * n + i])); mx = std::max(mx, fabs(hr[(size_t)j * n + i])); }
+  const double fl = TRI ? (double)n * (n + 1) * K : 2.0 * n * n * K;  // tri: useful flops of the triangle
+  printf("%-34s n=%d K=%d blocks=%6d  best %.3f ms avg %.3f  %.1f TF/s  relerr %.1e\n", name, n, K, nblk, best,
+         tot / reps, fl / best / 1e9, err / mx);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+void run2(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps, int grid = 0) {
+  const int ti = n / BM, tj = n / BN;
+  const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
+  auto launch = [&]() {
+    hipLaunchKernelGGL((k_gemm2<BM, BN, WM, WN, BK, TRI, SGB>), dim3(grid ? grid : nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti, nblk);
+  };
+  CK(hipMemset(C, 0, (size_t)n * n * 8));
+  launch();
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+  float best = 1e30, tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    hipEventRecord(a); launch(); hipEventRecord(b); hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b); best = std::min(best, ms); tot += ms;
+  }
+  // check a sample of columns
+  std::vector<double> hc((size_t)n * n), hr((size_t)n * n);
+  CK(hipMemcpy(hc.data(), C, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hr.data(), R, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  double err = 0, mx = 0;
+  for (int j = 0; j < n; j += 97)
+    for (int i = TRI ? j : 0; i < n; ++i) { err = std::max(err, fabs(hc[(size_t)j * n + i] - hr[(size_t)j * n + i])); mx = std::max(mx, fabs(hr[(size_t)j * n + i])); }
+  const double fl = TRI ? (double)n * (n + 1) * K : 2.0 * n * n * K;  // tri: useful flops of the triangle
+  printf("%-34s n=%d K=%d blocks=%6d  best %.3f ms avg %.3f  %.1f TF/s  relerr %.1e\n", name, n, K, nblk, best,
+         tot / reps, fl / best / 1e9, err / mx);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, bool TRI>
+void run3(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps, int grid = 0) {
+  const int ti = n / BM, tj = n / BN;
+  const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
+  auto launch = [&]() {
+    hipLaunchKernelGGL((k_gemm3<BM, BN, BK, TRI>), dim3(grid ? grid : nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti, nblk);
   };
   CK(hipMemset(C, 0, (size_t)n * n * 8));
   launch();
@@ -183,12 +430,11 @@ int main(int argc, char** argv) {
   double* w; CK(hipMalloc(&w, (size_t)K * 8));
   { std::vector<double> hw(K, 1.5); CK(hipMemcpy(w, hw.data(), K * 8, hipMemcpyHostToDevice)); }
   runlib("lib tri remap", n, K, true, false, 1, X, C, R, w, reps);
-  runlib("lib tri remap beta1", n, K, true, false, 1, X, C, R, w, reps, 0, 1.0);
-  runlib("lib persist224 remap", n, K, true, false, 1, X, C, R, w, reps, 224);
-  runlib("lib persist224 noremap", n, K, true, false, 0, X, C, R, w, reps, 224);
-  runlib("lib persist224 remap beta1", n, K, true, false, 1, X, C, R, w, reps, 224, 1.0);
-  runlib("lib persist224 noremap beta1", n, K, true, false, 0, X, C, R, w, reps, 224, 1.0);
-  runlib("lib persist256 noremap beta1", n, K, true, false, 0, X, C, R, w, reps, 256, 1.0);
-  run<128, 128, 2, 4, 16, true, 2200>("lab w2x4 pad persist224", n, K, X, X, C, R, reps, 224);
+  run<128, 128, 2, 2, 16, true>("lab 128x128 w2x2 bk16 tri", n, K, X, X, C, R, reps);
+  run2<128, 128, 2, 2, 16, true, 0>("lab2 128x128 w2x2 bk16 tri", n, K, X, X, C, R, reps);
+  run3<128, 128, 2, 2, 16, true>("lab3 dma 128x128 bk16 tri", n, K, X, X, C, R, reps);
+  run3<128, 128, 2, 2, 32, true>("lab3 dma 128x128 bk32 tri", n, K, X, X, C, R, reps);
+  run2<128, 128, 2, 2, 16, false, 0>("lab2 128x128 w2x2 bk16 full", n, K, X, X, C, R, reps);
+  run3<128, 128, 2, 2, 16, false>("lab3 dma 128x128 bk16 full", n, K, X, X, C, R, reps);
   return 0;
 }
