@@ -1032,7 +1032,9 @@ struct RoleTrace {
 #define ROLE(r) ((void)0)
 #endif
 
-template <bool VEC>
+// FASTS: every trailing tile of this launch is a full 128-tile (K = 256): they run the
+// branch-free slab loop (mfma_tile LOOP 1) -- one instantiation per kernel, as the allocator needs
+template <bool VEC, bool FASTS = false>
 __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ BlockSmem sm;
   __shared__ int sticket, sflag;
@@ -1351,10 +1353,10 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         const int64_t st = v - 1, u = st - b.s_full;
         const int sp = u < 0 ? 0 : ((u & 1) ? 2 : 1);
         const int64_t p = u < 0 ? 0 : (u >> 1);
-        // (the branch-free slab loop of the KKT SYRK is not used here: inside this kernel it raised
-        // the SGPR spills 89 -> 621 and the factorisation took 2.5 % longer)
-        mfma_tile<128, false, VEC, 2, false>(b.s, u < 0 ? st : b.s_full + p, sm.g128, sp, b.sscr + p * (128 * 128),
-                                             b.sflag + p);
+        // (both loops in one kernel raised the SGPR spills 89 -> 621 and cost 2.5 %: the launch
+        // picks the kernel instead, FASTS)
+        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0>(
+            b.s, u < 0 ? st : b.s_full + p, sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
       }
     }
   }
@@ -1603,8 +1605,13 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       b.gs_total = b.gs_cum[b.ngs];
     }
     const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
-    if (vec) hipLaunchKernelGGL(k_potrf_block<true>, dim3((unsigned)grid), dim3(256), 0, st, b);
-    else hipLaunchKernelGGL(k_potrf_block<false>, dim3((unsigned)grid), dim3(256), 0, st, b);
+    // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
+    // branch-free tile loop (IPM_FASTS=0: never)
+    static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
+    const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
+    if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    else if (vec) hipLaunchKernelGGL((k_potrf_block<true, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((k_potrf_block<false, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
   }
 }
 
