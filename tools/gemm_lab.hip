@@ -211,6 +211,100 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm2(int n, int K, const doub
   }
 }
 
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+__global__ __launch_bounds__(WM * WN * 64, 2) void k_gemm4(int n, int K, const double* __restrict__ X, int ldx,
+                                                        const double* __restrict__ Y, int ldy,
+                                                        double* __restrict__ C, int ldc, int tiles_i, int nblk) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int LX = BM + 16, LY = BN + 16;
+  constexpr int PX = BK * BM / NT, PY = BK * BN / NT;
+  __shared__ double sX[2][BK * LX];
+  __shared__ double sY[2][BK * LY];
+  for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
+  int bi, bj;
+  if (TRI) {
+    const int L = Lp;
+    int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= L) ++b;
+    while (b * (b + 1) / 2 > L) --b;
+    bi = b; bj = L - b * (b + 1) / 2;
+  } else {
+    bi = Lp % tiles_i; bj = Lp / tiles_i;
+  }
+  const int I0 = bi * BM, J0 = bj * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv % WM, wj = wv / WM;
+  dbl4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = dbl4{0, 0, 0, 0};
+  constexpr int TPRX = BM / PX, TPRY = BN / PY;
+  const int xr = tid / TPRX, xc = (tid % TPRX) * PX;
+  const int yr = tid / TPRY, yc = (tid % TPRY) * PY;
+  double rx[PX], ry[PY];
+  const double* xb = X + (size_t)xr * ldx + I0 + xc;
+  const double* yb = Y + (size_t)yr * ldy + J0 + yc;
+  auto gload = [&](int s) {
+    const double2* xp = reinterpret_cast<const double2*>(xb + (size_t)s * BK * ldx);
+    const double2* yp = reinterpret_cast<const double2*>(yb + (size_t)s * BK * ldy);
+#pragma unroll
+    for (int q = 0; q < PX / 2; ++q) { double2 v = xp[q]; rx[2 * q] = v.x; rx[2 * q + 1] = v.y; }
+#pragma unroll
+    for (int q = 0; q < PY / 2; ++q) { double2 v = yp[q]; ry[2 * q] = v.x; ry[2 * q + 1] = v.y; }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < PX; ++q) sX[buf][xr * LX + xc + q] = rx[q];
+#pragma unroll
+    for (int q = 0; q < PY; ++q) sY[buf][yr * LY + yc + q] = ry[q];
+  };
+  const int nslab = K / BK;
+  gload(0); sstore(0);
+  gload(nslab > 1 ? 1 : 0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < nslab; ++s) {
+    const int buf = s & 1;
+    const double* bx = sX[buf];
+    const double* by = sY[buf];
+    // SGB 2: the whole slab's operand fragments first (all 4 k-steps), then the stores / loads of
+    // the next slabs, then the 64 MFMAs from registers
+    double a[BK / 4][TN], b[BK / 4][TM];
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) a[kk][t] = by[(kk * 4 + fk) * LY + wj * (BN / WN) + t * 16 + fr];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) b[kk][t] = bx[(kk * 4 + fk) * LX + wi * (BM / WM) + t * 16 + fr];
+    }
+    sstore(buf ^ 1);
+    gload(min(s + 2, nslab - 1));
+    if (SGB == 2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk)
+#pragma unroll
+      for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TM; ++ti) acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk][tj], b[kk][ti], acc[tj][ti], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int tj = 0; tj < TN; ++tj)
+#pragma unroll
+    for (int ti = 0; ti < TM; ++ti) {
+      const int i = I0 + wi * (BM / WM) + ti * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = J0 + wj * (BN / WN) + tj * 16 + fk + 4 * r;
+        if (!TRI || i >= j) C[(size_t)j * ldc + i] = acc[tj][ti][r];
+      }
+    }
+  __syncthreads();
+  }
+}
+
 // k_gemm2 with the slabs brought into LDS by the load itself (global_load_lds, 16 bytes per lane:
 // one wave instruction = one 128-double slab row): no register staging, no LDS store
 // instructions.  One slab of prefetch (the DMA of slab s+1 runs under slab s's MFMAs).
@@ -388,6 +482,34 @@ void run3(const char* name, int n, int K, double* X, double* Y, double* C, doubl
          tot / reps, fl / best / 1e9, err / mx);
 }
 
+template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+void run4(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps, int grid = 0) {
+  const int ti = n / BM, tj = n / BN;
+  const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
+  auto launch = [&]() {
+    hipLaunchKernelGGL((k_gemm4<BM, BN, WM, WN, BK, TRI, SGB>), dim3(grid ? grid : nblk), dim3(WM * WN * 64), 0, 0, n, K, X, n, Y, n, C, n, ti, nblk);
+  };
+  CK(hipMemset(C, 0, (size_t)n * n * 8));
+  launch();
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+  float best = 1e30, tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    hipEventRecord(a); launch(); hipEventRecord(b); hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b); best = std::min(best, ms); tot += ms;
+  }
+  // check a sample of columns
+  std::vector<double> hc((size_t)n * n), hr((size_t)n * n);
+  CK(hipMemcpy(hc.data(), C, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hr.data(), R, (size_t)n * n * 8, hipMemcpyDeviceToHost));
+  double err = 0, mx = 0;
+  for (int j = 0; j < n; j += 97)
+    for (int i = TRI ? j : 0; i < n; ++i) { err = std::max(err, fabs(hc[(size_t)j * n + i] - hr[(size_t)j * n + i])); mx = std::max(mx, fabs(hr[(size_t)j * n + i])); }
+  const double fl = TRI ? (double)n * (n + 1) * K : 2.0 * n * n * K;  // tri: useful flops of the triangle
+  printf("%-34s n=%d K=%d blocks=%6d  best %.3f ms avg %.3f  %.1f TF/s  relerr %.1e\n", name, n, K, nblk, best,
+         tot / reps, fl / best / 1e9, err / mx);
+}
+
 void runlib(const char* name, int n, int K, bool tri, bool weight, int remap, double* X, double* C, double* R,
             double* w, int reps, int persist = 0, double beta = 0.0) {
   ipm::GemmArgs a;
@@ -430,11 +552,11 @@ int main(int argc, char** argv) {
   double* w; CK(hipMalloc(&w, (size_t)K * 8));
   { std::vector<double> hw(K, 1.5); CK(hipMemcpy(w, hw.data(), K * 8, hipMemcpyHostToDevice)); }
   runlib("lib tri remap", n, K, true, false, 1, X, C, R, w, reps);
-  run<128, 128, 2, 2, 16, true>("lab 128x128 w2x2 bk16 tri", n, K, X, X, C, R, reps);
   run2<128, 128, 2, 2, 16, true, 0>("lab2 128x128 w2x2 bk16 tri", n, K, X, X, C, R, reps);
-  run3<128, 128, 2, 2, 16, true>("lab3 dma 128x128 bk16 tri", n, K, X, X, C, R, reps);
-  run3<128, 128, 2, 2, 32, true>("lab3 dma 128x128 bk32 tri", n, K, X, X, C, R, reps);
+  run4<128, 128, 2, 2, 16, true, 0>("lab4 reads-first tri", n, K, X, X, C, R, reps);
+  run4<128, 128, 2, 2, 16, true, 2>("lab4 reads-first+sb tri", n, K, X, X, C, R, reps);
   run2<128, 128, 2, 2, 16, false, 0>("lab2 128x128 w2x2 bk16 full", n, K, X, X, C, R, reps);
-  run3<128, 128, 2, 2, 16, false>("lab3 dma 128x128 bk16 full", n, K, X, X, C, R, reps);
+  run4<128, 128, 2, 2, 16, false, 0>("lab4 reads-first full", n, K, X, X, C, R, reps);
+  run4<128, 128, 2, 2, 16, false, 2>("lab4 reads-first+sb full", n, K, X, X, C, R, reps);
   return 0;
 }
