@@ -388,6 +388,18 @@ def lstsq_singular():
                                                             linear_solve_method=meth))
 
 
+def eq_ineq_methods():
+    """lp_eq_ineq (dense infeasible start + phase 1) under np_solve / direct / np_lstsq: the steps
+    near t ~ 1e7 have a nearly singular H, so the reference's own spread decides the bar."""
+    for meth in ("np_lstsq",):
+        rng = np.random.default_rng(6)
+        n = 80
+        Aeq = rng.uniform(-2, 2, (20, n)); C = rng.uniform(-2, 2, (10, n)); xf = rng.uniform(-2, 2, n)
+        run_solve(f"meth_lp_eq_ineq_{meth}", RefLP, dict(c=rng.uniform(-2, 2, n), A=Aeq, b=Aeq @ xf, C=C,
+                                                         d=C @ xf + 1, lower_bound=-3, upper_bound=3,
+                                                         **problems.LP_KWARGS, linear_solve_method=meth))
+
+
 if __name__ == "__main__":
     _wrap_feasible()
     if sys.argv[1:] == ["extra"]:
@@ -396,6 +408,8 @@ if __name__ == "__main__":
         eq_many()
     elif sys.argv[1:] == ["npy_lp"]:
         npy_lp()
+    elif sys.argv[1:] == ["eq_ineq_methods"]:
+        eq_ineq_methods()
     elif sys.argv[1:] == ["lstsq_singular"]:
         lstsq_singular()
     elif sys.argv[1:] == ["eq_box_stable"]:
