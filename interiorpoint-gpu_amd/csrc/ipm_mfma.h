@@ -112,7 +112,8 @@ struct alignas(16) MfSmem {
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false, bool SPLITADD = false,
           int LOOP = 0>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
-                                          double* part = nullptr, unsigned* pflag = nullptr) {
+                                          double* part = nullptr, unsigned* pflag = nullptr, int64_t kb = -1,
+                                          int64_t ke = -1) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
   auto& sX = sm.sX;
@@ -142,14 +143,16 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wi = wv & 1, wj = wv >> 1;
   const int sr = tid / TPR, sc = (tid % TPR) * PT;
-  const int64_t kbeg = SPLIT == 1 ? a.K / 2 : 0;
+  // SPLITADD with kb >= 0: SPLIT 1 is the K piece [kb, ke) of a stream-K tail (k_mfma_gemm_streamk)
+  const bool kpiece = SPLITADD && kb >= 0;
+  const int64_t kbeg = SPLIT == 1 ? (kpiece ? kb : a.K / 2) : 0;
   const double* xp = a.X + (sr + kbeg) * a.ldx + I0 + sc;
   const double* yp = a.Y + (sr + kbeg) * a.ldy + J0 + sc;
   const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
   // K extent of this tile (the KKT SYRK with deferred slices: columns ahead take fewer k rows)
   int kt32 = (int)a.K;
   if (a.kend256) kt32 = __builtin_amdgcn_readfirstlane(std::min(kt32, a.kend256[J0 >> 8]));
-  if (SPLIT == 1) kt32 = kt32 - kt32 / 2;
+  if (SPLIT == 1) kt32 = kpiece ? (int)(ke - kb) : kt32 - kt32 / 2;
   if (SPLIT == 2) kt32 = kt32 / 2;
   const int64_t Kt = kt32;
   const int64_t nslab = (Kt + BK - 1) / BK;
@@ -424,6 +427,132 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t 
     mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, s_full + p, sm, (u & 1) ? 2 : 1, part, sflag + p);
 }
 
+// Stream-K tail (the KKT SYRK on 128-tiles): a lower-triangle grid of nt = R * slots + q tiles
+// runs R whole rounds, and its last q tiles as P K pieces each (q * P <= slots), so that the
+// partial last round becomes one short round of pieces on (nearly) every slot instead of q whole
+// tiles on q slots (2080 tiles on 512 slots: 4 rounds + 512 pieces of K/16).  Blocks [0, npc)
+// are the pieces, dispatched FIRST: piece u = tile s_full + u / P, K range [p Kp, min(K, p Kp +
+// Kp)), p = u % P; its partial goes to sscr + u * BM * BM (sc1).  The piece that arrives last at
+// the tile's counter (cnt[u / P], zeroed before the launch) sums the P partials in the fixed
+// order p = 0 .. P-1 and applies the epilogue: deterministic, and nobody waits.  Blocks
+// [npc, npc + s_full) are the whole tiles.
+template <int BM>
+__device__ __forceinline__ void tile_ij(const GemmArgs& a, int64_t Lw, int64_t& bi, int64_t& bj) {
+  int64_t L = Lw;
+  const int64_t q = a.nblk >> 3;
+  if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);
+  if (a.rowmajor) {
+    bi = L / a.tiles_j;
+    bj = L % a.tiles_j;
+  } else if (a.tri) {
+    int64_t b = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while ((b + 1) * (b + 2) / 2 <= L) ++b;
+    while (b * (b + 1) / 2 > L) --b;
+    bi = b;
+    bj = L - b * (b + 1) / 2;
+  } else {
+    bi = L % a.tiles_i;
+    bj = L / a.tiles_i;
+  }
+}
+
+template <bool WEIGHT, bool VEC>
+__global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_t s_full, int P, int64_t Kp,
+                                                              int64_t npc, double* sscr, unsigned* cnt,
+                                                              int pieces_last) {
+  constexpr int BM = 128;
+  if (a.info && *a.info != 0) return;
+  __shared__ MfSmem<BM, 2> sm;
+  __shared__ int slast;
+  int64_t b = blockIdx.x;
+  constexpr int FL = VEC ? 1 : 0;
+  // block order: pieces first (default) or whole tiles first
+  bool whole;
+  if (pieces_last) {
+    whole = b < s_full;
+    if (!whole) b -= s_full;
+  } else {
+    whole = b >= npc;
+  }
+  if (whole) {
+    const int64_t L = pieces_last ? b : b - npc;
+    if (FL && tile_fast_ok<BM>(a, L)) mfma_tile<BM, WEIGHT, VEC, 2, false, false, true, FL>(a, L, sm);
+    else mfma_tile<BM, WEIGHT, VEC, 2, false, false, true>(a, L, sm);
+    return;
+  }
+  const int64_t ti = b / P, p = b - ti * P, L = s_full + ti;
+  const int64_t k0 = p * Kp, k1 = std::min<int64_t>(a.K, k0 + Kp);
+  double* part = sscr + b * (int64_t)(BM * BM);
+  // (the flag mfma_tile raises after its partial: a per-piece word past the tile counters)
+  unsigned* pf = cnt + (a.nblk - s_full) + b;
+  if (FL && (k0 % 16) == 0 && ((k1 - k0) % 16) == 0 && tile_fast_ok<BM>(a, L))
+    mfma_tile<BM, WEIGHT, VEC, 2, false, false, true, FL>(a, L, sm, 1, part, pf, k0, k1);
+  else
+    mfma_tile<BM, WEIGHT, VEC, 2, false, false, true>(a, L, sm, 1, part, pf, k0, k1);
+  // (mfma_tile ended with s_waitcnt vmcnt(0) + barrier after the partial's sc1 stores)
+  const int tid = threadIdx.x;
+  if (tid == 0)
+    slast = __hip_atomic_fetch_add(&cnt[ti], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(P - 1);
+  __syncthreads();
+  if (!slast) return;
+  int64_t bi, bj;
+  tile_ij<BM>(a, L, bi, bj);
+  const int64_t I0 = bi * BM, J0 = bj * BM;
+  const bool cinit = a.sub || a.accum || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
+  const double* base = sscr + ti * P * (int64_t)(BM * BM);
+  // column-major tile: consecutive threads take consecutive i (coalesced partial and C traffic)
+  for (int e = tid; e < BM * BM; e += 256) {
+    const int il = e & (BM - 1), jl = e / BM;
+    const int64_t i = I0 + il, j = J0 + jl;
+    if (i >= a.ni || j >= a.nj || (a.tri && i < j)) continue;
+    // all P partial loads in flight at once (P <= 16), then the fixed-order sum
+    double pv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pv[q] = q < P ? ld_sc1(&base[q * (int64_t)(BM * BM) + e]) : 0.0;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q < P) s += pv[q];
+    double* cp = a.C + j * a.ldc + i;
+    if (cinit) {
+      *cp = *cp + s;
+    } else {
+      double v = a.alpha * s;
+      if (a.beta != 0.0) v += a.beta * (*cp);
+      if (a.P) v += a.tP * a.P[j * a.ldp + i];
+      if (a.dvec && i == j) v += a.dvec[i];
+      *cp = v;
+    }
+  }
+}
+
+// stream-K plan for nt 128-tiles on `slots` slots: pieces per tile P (0: not worth it) and the
+// piece length Kp (whole 16-row slabs); the last piece of a tile may be shorter
+// IPM_STREAMK: 0 off (the K-halves split tail; default), 1 pieces first, 2 pieces last,
+// 3 pieces first with at most 8 pieces per tile
+inline int streamk_mode() {
+  static const int mode = [] {
+    const char* e = getenv("IPM_STREAMK");
+    return e ? atoi(e) : 0;
+  }();
+  return mode;
+}
+inline int streamk_plan(int64_t nt, int slots, int64_t cap, int64_t K, int64_t& q, int64_t& Kp) {
+  const int mode = streamk_mode();
+  q = 0;
+  Kp = 0;
+  if (!mode || slots <= 0 || nt < slots) return 0;
+  q = nt % slots;
+  if (q == 0) return 0;
+  const int pmax = mode == 3 ? 8 : 16;
+  int P = 1;
+  while (P * 2 <= pmax && q * P * 2 <= slots && q * P * 2 <= cap && K / (P * 2) >= 64) P *= 2;
+  if (P < 4) return 0;
+  Kp = ((K + P - 1) / P + 15) / 16 * 16;
+  P = (int)((K + Kp - 1) / Kp);
+  return P >= 4 ? P : 0;
+}
+
 // how many of nt tiles to split: list schedule on `slots` workgroup slots (2 per CU), whole tile
 // 1.0, half tile 0.55; the q with the smallest makespan (cached per grid)
 inline int64_t gemm_split_plan(int64_t nt, int slots, int64_t cap) {
@@ -514,7 +643,29 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
   const int64_t ti = (a.ni + BM - 1) / BM, tj = (a.nj + BM - 1) / BM;
   a.tiles_i = ti;
   a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
-  const int64_t q = ws ? gemm_split_plan(a.nblk, slots, cap) : 0;
+  if (BM == 128 && ws) {
+    int64_t qk = 0, Kp = 0;
+    const int P = streamk_plan(a.nblk, slots, cap, a.K, qk, Kp);
+    if (P > 0) {
+      const int64_t s_full = a.nblk - qk, npc = qk * P;
+      // counters: qk tile words, then npc per-piece words (ws has cap * 128 * 128 doubles of
+      // partials, then the flag area)
+      unsigned* cnt = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
+      hipMemsetAsync(cnt, 0, (qk + npc) * sizeof(unsigned), st);
+      dim3 g((unsigned)(npc + s_full)), blk(256);
+      const int pl = streamk_mode() == 2 ? 1 : 0;
+      if (a.w) {
+        if (vec) hipLaunchKernelGGL((k_mfma_gemm_streamk<true, true>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
+        else hipLaunchKernelGGL((k_mfma_gemm_streamk<true, false>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
+      } else {
+        if (vec) hipLaunchKernelGGL((k_mfma_gemm_streamk<false, true>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
+        else hipLaunchKernelGGL((k_mfma_gemm_streamk<false, false>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
+      }
+      return;
+    }
+  }
+  // (the K-halves planner keeps its round-2 cap of 256 tiles)
+  const int64_t q = ws ? gemm_split_plan(a.nblk, slots, std::min<int64_t>(cap, 256)) : 0;
   if (q == 0) {
     if (BM == 128) mfma_gemm_launch_bm<128>(st, a, vec);
     else mfma_gemm_launch_bm<64>(st, a, vec);

@@ -12,10 +12,13 @@ EPS = np.finfo(np.float64).eps
 
 
 @pytest.mark.parametrize("k,n", [(4, 16), (1, 1), (16, 128), (37, 130), (300, 257), (512, 1024), (0, 5),
-                                 (2050, 700), (64, 1000), (2048, 8192)])
+                                 (2050, 700), (64, 1000), (2048, 8192), (2050, 8100), (600, 10000)])
 def test_syrk_weighted_matches_numpy(k, n):
     """Includes grids whose tail runs as split K halves (k_mfma_gemm_split: n = 1000 and 1024 on
-    64-tiles -- every tile split, ragged edge tiles included -- and 8192 on 128-tiles)."""
+    64-tiles -- every tile split, ragged edge tiles included) and as stream-K pieces
+    (k_mfma_gemm_streamk on 128-tiles: n = 8192, K = 2048 -> 32 tail tiles x 16 pieces; n = 8100,
+    K = 2050 -> ragged edge tiles and a ragged last piece; n = 10000, K = 600 -> 3160 tiles,
+    88 tail tiles x 4 pieces of 160 / 120 rows)."""
     rng = np.random.default_rng(k * 1000 + n)
     X = rng.uniform(-2, 2, (k, n))
     w = rng.uniform(0.1, 3, k)
