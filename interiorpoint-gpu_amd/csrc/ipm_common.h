@@ -61,7 +61,7 @@ struct SyrkEpi {
 // workspace of the split tail for an n x n lower-triangle SYRK: the cap and its size in doubles
 inline int64_t syrk_split_cap(int64_t n) {
   const int64_t T = (n + 63) / 64;   // 64-tile grid (the launcher uses 64-tiles below 768 128-tiles)
-  return std::min<int64_t>(512, std::max<int64_t>(T * (T + 1) / 2, 8));
+  return std::min<int64_t>(256, std::max<int64_t>(T * (T + 1) / 2, 8));
 }
 // (flag area: 2c + 4 words -- the stream-K tail's tile counters and per-piece words)
 inline int64_t syrk_split_ws_doubles(int64_t n) {

@@ -528,12 +528,13 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
 
 // stream-K plan for nt 128-tiles on `slots` slots: pieces per tile P (0: not worth it) and the
 // piece length Kp (whole 16-row slabs); the last piece of a tile may be shorter
-// IPM_STREAMK: 0 off (the K-halves split tail; default), 1 pieces first, 2 pieces last,
-// 3 pieces first with at most 8 pieces per tile
+// IPM_STREAMK: 0 off (the K-halves split tail), 1 pieces first, 2 pieces last,
+// 3 pieces first with at most 8 pieces per tile (default: 2.37 -> 2.30 ms at n = 8192, K = 2048,
+// 2.63 -> 2.51 ms at n = 8100, K = 2050; profiles/r2_streamk_ab.txt)
 inline int streamk_mode() {
   static const int mode = [] {
     const char* e = getenv("IPM_STREAMK");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 3;
   }();
   return mode;
 }
