@@ -33,4 +33,4 @@ for c in FETCH_SIZE WRITE_SIZE "$MF"; do
 done
 P=$(find $OUT/pmc_1 $OUT/pmc_2 $OUT/pmc_3 -name '*counter_collection.csv' | tr '\n' ' ')
 python3 scripts/pmc_summary.py "k_potrf_block" $OUT/pmc_potrf_block.json ${PMC_N:-8192} ${PMC_M:-2048} $P
-python3 scripts/pmc_summary.py "k_mfma_gemm<128, true, true" $OUT/pmc_kkt_syrk.json ${PMC_N:-8192} ${PMC_M:-2048} $P
+python3 scripts/pmc_summary.py "k_mfma_gemm_streamk<true, true" $OUT/pmc_kkt_syrk.json ${PMC_N:-8192} ${PMC_M:-2048} $P

@@ -16,9 +16,9 @@ EPS = np.finfo(np.float64).eps
 def test_syrk_weighted_matches_numpy(k, n):
     """Includes grids whose tail runs as split K halves (k_mfma_gemm_split: n = 1000 and 1024 on
     64-tiles -- every tile split, ragged edge tiles included) and as stream-K pieces
-    (k_mfma_gemm_streamk on 128-tiles: n = 8192, K = 2048 -> 32 tail tiles x 16 pieces; n = 8100,
-    K = 2050 -> ragged edge tiles and a ragged last piece; n = 10000, K = 600 -> 3160 tiles,
-    88 tail tiles x 4 pieces of 160 / 120 rows)."""
+    (k_mfma_gemm_streamk on 128-tiles, default IPM_STREAMK=3: n = 8192, K = 2048 -> 32 tail tiles
+    x 8 pieces; n = 8100, K = 2050 -> ragged edge tiles and a ragged last piece; n = 10000, K = 600
+    -> 3160 tiles, 88 tail tiles: too many for the 256 partial slots, so the K-halves split runs)."""
     rng = np.random.default_rng(k * 1000 + n)
     X = rng.uniform(-2, 2, (k, n))
     w = rng.uniform(0.1, 3, k)
