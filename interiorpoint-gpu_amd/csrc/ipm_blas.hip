@@ -2164,6 +2164,7 @@ __global__ __launch_bounds__(512, 1) void k_trinv128(int64_t n, const double* __
 // Hand-off as k_trsv_chain (sc1 stores, vmcnt(0), progress word; consumers poll and read with
 // sc1 loads).
 // -------------------------------------------------------------------------------------
+constexpr long long TRSV_PENDING = -1LL;   // 0xFFFF...F: y's content before its block is solved
 struct Trsv128Smem {
   double sX[TB2 * (TB2 + 1)];   // X_B, X[c][r] at r * 129 + c
   double sx[TB2];               // x_{B+1}
@@ -2268,10 +2269,20 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
     if (t > 0) {
       const int64_t k0 = r0 + TB2;
       const int krows = (int)min((int64_t)TB2, n - k0);
-      if (tid == 0)
-        while (ld_ctl(&ctl[1]) < (unsigned)t) __builtin_amdgcn_s_sleep(1);
-      __syncthreads();
-      if (tid < TB2) sm.sx[tid] = tid < krows ? ld_sc1(y + k0 + tid) : 0.0;
+      // x_{B+1} is polled directly (y starts as the all-ones NaN pattern, which no fp64 operation
+      // produces): no progress-word round trip on the chain.  Bounded, so a missing producer ends
+      // in a wrong result instead of a hang.
+      if (tid < TB2) {
+        double v = 0.0;
+        if (tid < krows) {
+          for (unsigned spin = 0;; ++spin) {
+            v = ld_sc1(y + k0 + tid);
+            if (__double_as_longlong(v) != TRSV_PENDING || spin > (1u << 20)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        sm.sx[tid] = v;
+      }
       __syncthreads();
       double p = 0.0, p2 = 0.0;
 #pragma unroll
@@ -2331,6 +2342,7 @@ void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const
   const int nblk = (int)cdiv(n, TB2);
   hipLaunchKernelGGL(k_trinv128, dim3(nblk), dim3(512), 0, st, n, L, ldl, xinv_ws);
   const int grid = std::min(nblk, 256);
+  hipMemsetAsync(x, 0xFF, n * sizeof(double), st);   // TRSV_PENDING in every row
   hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl);
 }
 
