@@ -88,6 +88,48 @@ def potrf_flops(N):
     return N ** 3 / 3 + N ** 2 / 2 + N / 6
 
 
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def fixture_parity(s, seg, seed, args, k):
+    """The bench's rank-0 instance IS the reference fixture instance (seed 0, n=8192, m=2048, grid
+    values): compare the K timed Newton steps' sizes and the iterate after them with the reference
+    run (tests/golden/m3_qp_full.npz phase-1 steps / m3_qp_feas.npz barrier steps; x_snap_K is the
+    reference iterate handed to its (K+1)-th line search).  None when no fixture covers the run."""
+    if seed != 0 or args.instances != 1 or args.problem != "qp" or (args.n, args.m) != (8192, 2048):
+        return None
+    name = {"phase1": "m3_qp_full", "barrier": "m3_qp_feas"}[seg]
+    path = os.path.join(GOLDEN, name + ".npz")
+    if not os.path.exists(path):
+        name = {"phase1": "m3_qp_ph1", "barrier": "m3_qp_feas"}[seg]
+        path = os.path.join(GOLDEN, name + ".npz")
+        if not os.path.exists(path):
+            return None
+    z = np.load(path, allow_pickle=False)
+    p1 = s.phase1_solver
+    tr = list(p1.phase1_ns.trace) if (seg == "phase1" and p1 is not None) else list(s.ns.trace)
+    steps = np.array([t[0] for t in tr])
+    ref = z["trace_step"][:len(steps)]
+    out = {"fixture": name, "newton_steps": int(len(steps)), "steps_identical": bool(np.array_equal(steps, ref))}
+    key = f"x_snap_{k}"
+    if key in z.files:
+        x = (p1.x if seg == "phase1" else s.x_last).cpu().numpy()
+        xr = z[key]
+        if x.shape == xr.shape:
+            out["x_rel_err"] = float(np.linalg.norm(x - xr) / np.linalg.norm(xr))
+    return out
+
+
+def hbm_kernels(prob):
+    """HIP-event GB/s of the HBM-bound kernels of one Newton step (engine ipm_time_hbm_kernels)."""
+    try:
+        t = prob.time_hbm_kernels(20)
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal to the bench line
+        return {"error": str(e)}
+    return {k: {"ms": ms, "bytes": by, "GB/s": by / (ms * 1e-3) / 1e9, "frac_of_hbm_peak": by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            for k, (ms, by) in t.items()}
+
+
 def launch_ranks(n):
     """Parent of a self-launched N-rank run: no GPU call happens here (device_count does not
     initialise the runtime on this image); each child is a fresh process owning LOCAL_RANK."""
@@ -261,7 +303,7 @@ def main():
     with on(streams[0]):
         h = L.Handle.get(dev_index)
     import ctypes
-    res = {}
+    res, evidence, hbm_rates = {}, {}, {}
     for name, budget in segs:
         if budget <= 0:
             res[name] = dict(iters=0, seconds=0.0, kkt_ms=0.0, potrf_ms=0.0, kkt_flops=0.0, N=0)
@@ -300,6 +342,12 @@ def main():
             iters += sum(s.inner_iters) + (sum(p1.inner_iters) if p1 is not None and name == "phase1" else 0)
         res[name] = dict(iters=float(iters), seconds=el, kkt_ms=a.value, potrf_ms=b.value, kkt_flops=kkt_flops,
                          N=args.n + (1 if name == "phase1" else 0))
+        if rank == 0:
+            # after the timed region: rank 0's own evidence (trace/iterate vs the reference fixture,
+            # HBM-kernel GB/s on this solver's buffers)
+            evidence[name] = fixture_parity(solvers[0], name, seeds[0], args, budget)
+            if args.problem in ("qp", "lp"):
+                hbm_rates[name] = hbm_kernels(fm0.prob)
         del solvers
 
     keys = ("iters", "seconds", "kkt_ms", "potrf_ms")
@@ -379,11 +427,22 @@ def main():
             "whole_iteration_fp64_frac": (f_iter * total_iters / world / tmax) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "newton_iters": total_iters,
             "lib_sha256": lib_digest(),
+            "parity": evidence,
+            "hbm_kernels": hbm_rates,
         }
-        if args.problem != "qp":
-            rec["metric"] = f"Newton iters/sec, dense {args.problem.upper()} (config {'3' if args.problem == 'lp' else '5'})"
-            rec["config"]["workload"] = rec["config"]["workload"].replace("QPSolver", Cls.__name__).replace(
-                "dense QP", "dense " + args.problem.upper())
+        if args.problem == "lp":
+            rec["metric"] = "Newton iters/sec, dense LP (config 3)"
+            rec["data"] = "synthetic (seeded M3-LP generator, testSolver.py:104-148 shapes; U(-2,2) on a 2^-10 grid)"
+            rec["config"]["workload"] = (f"LPSolver.solve() dense LP n={n}, m={m} ineq, box +-3, test_LP kwargs; per "
+                                         f"instance {k1} phase-1 iterations (from x0=0) + {args.steps - k1} "
+                                         f"barrier-phase iterations (from the feasible x_f)")
+        elif args.problem == "socp":
+            rec["metric"] = "Newton iters/sec, SOCP (config 5)"
+            rec["data"] = ("synthetic (seeded M5 generator: P=I, K cones of 16 Gaussian rows, d_i making x0 "
+                           "strictly feasible; no bounds)")
+            rec["config"]["workload"] = (f"SOCPSolver.solve() n={n}, {m} second-order cones of 16 rows, P=I, no "
+                                         f"bounds, test_SOCP kwargs; {args.steps} barrier-phase iterations from the "
+                                         f"strictly feasible x0 (phase 1 skipped)")
         if not args.no_cpu and world == 1 and args.problem == "qp":
             rec["cpu_baseline"] = cpu_baseline(insts[0][0], kwargs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

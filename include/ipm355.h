@@ -216,10 +216,26 @@ int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda
    averages (ms) over the Newton iterations since the reset, and their count */
 int ipm_set_timing(ipm_handle* h, int on);
 int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count);
+/* debug knob: the spin bound (in s_sleep(1) units) after which the persistent backward solve's
+   chain step stops waiting for its producer and raises its device error word; the Newton step's
+   readback then returns IPM_HIP_ERROR instead of using the step.  0 restores the default 2^20.
+   Process-wide; tests use a tiny bound to trip the error path once. */
+int ipm_debug_set_trsv_spin_limit(unsigned limit);
+/* debug knob: the backward-solve workgroup holding chain ticket `ticket` sleeps ~7 ms before
+   publishing its progress word (-1: off), so later tickets overtake it -- exercises the monotonic
+   progress publish.  Process-wide. */
+int ipm_debug_set_trsv_publish_delay(int ticket);
 /* KKT-SYRK flops of one Newton step of this problem (m n (n+1) in total), split between the
    up-front SYRK kernel and the k-row slices deferred into the Cholesky launches, where they fill
    the CUs the panel chain leaves idle (opt-in, IPM_DEFER=1) */
 int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred);
+/* measurement: HIP-event time (ms, averaged over `reps`, on the handle's stream) of the HBM-bound
+   kernels of one Newton step on this problem's buffers -- ms[0] the slack GEMV C x, ms[1] the
+   gradient GEMV C^T w, ms[2] one 64-candidate line-search pass over the S slacks.  Clobbers only
+   scratch.  LP/QP problems with inequality rows (bench.py reports them as GB/s). */
+int ipm_time_hbm_kernels(ipm_problem* pr, int reps, double* ms);
+/* out[0..2] = m (inequality rows), n, S (slacks incl. box bounds) */
+int ipm_problem_sizes(ipm_problem* pr, int64_t* out);
 
 /* ---- batched ADMM Lasso (LassoSolver.py) ------------------------------ *
  * S problems  min_x 1/(2m) ||A x - b_s||^2 + reg_s ||x||_1  solved together.  Every n x S matrix

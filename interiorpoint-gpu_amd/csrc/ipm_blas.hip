@@ -10,6 +10,7 @@
 // Reference call sites replaced: FunctionManager.py:123, 256-258, 301-306, 801-805
 // (cuBLAS gemv/gemm via CuPy); NewtonSolver.py:286-313 (cuSOLVER potrf + 2 trsv);
 // NewtonSolverInfeasibleStart.py:398-452 (potrf + trsm with p right-hand sides).
+#include <atomic>
 #include "ipm_common.h"
 #include <cstdio>
 #include "ipm_mfma.h"
@@ -2175,7 +2176,9 @@ struct Trsv128Smem {
 
 __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, const double* __restrict__ L,
                                                         int64_t ldl, const double* __restrict__ b, int64_t bstride,
-                                                        const double* __restrict__ Xws, double* y, unsigned* ctl) {
+                                                        const double* __restrict__ Xws, double* y, unsigned* ctl,
+                                                        unsigned* err, unsigned spin_limit,
+                                                        int delay_ticket) {
   __shared__ Trsv128Smem sm;
   __shared__ int sticket;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 8 waves
@@ -2269,15 +2272,21 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
     if (t > 0) {
       const int64_t k0 = r0 + TB2;
       const int krows = (int)min((int64_t)TB2, n - k0);
-      // x_{B+1} is polled directly (y starts as the all-ones NaN pattern, which no fp64 operation
-      // produces): no progress-word round trip on the chain.  Bounded, so a missing producer ends
-      // in a wrong result instead of a hang.
+      // x_{B+1} is polled directly (y starts as the all-ones NaN pattern, which no fp64 arithmetic
+      // produces -- b must not hold it either, trsv_lower_t's contract): no progress-word round trip
+      // on the chain.  The spin is bounded: a producer that has not published after spin_limit
+      // sleeps raises the sticky device error word *err (bit 0), which the host reads with the
+      // Newton step's readback and turns into IPM_HIP_ERROR -- the step is never used silently.
       if (tid < TB2) {
         double v = 0.0;
         if (tid < krows) {
           for (unsigned spin = 0;; ++spin) {
             v = ld_sc1(y + k0 + tid);
-            if (__double_as_longlong(v) != TRSV_PENDING || spin > (1u << 20)) break;
+            if (__double_as_longlong(v) != TRSV_PENDING) break;
+            if (spin >= spin_limit) {
+              __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
             __builtin_amdgcn_s_sleep(1);
           }
         }
@@ -2313,7 +2322,13 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
       st_sc1(y + r0 + c, (sm.spart[0][c] + sm.spart[1][c]) + (sm.spart[2][c] + sm.spart[3][c]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(&ctl[1], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // publish "tickets <= t solved": monotonic.  With the data-polled chain a later ticket can finish
+    // (it only needs x_{B+1}, which it read from y) before this store lands; a plain store could
+    // then move ctl[1] backwards and leave the pre loop above waiting forever.
+    if (t == delay_ticket) {   // debug knob: a late publisher (tests the monotonic publish)
+      for (int i = 0; i < 2000; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+    if (tid == 0) __hip_atomic_fetch_max(&ctl[1], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
   }
 }
@@ -2328,14 +2343,19 @@ static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int
     hipLaunchKernelGGL(k_trsv_chain<false>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, bstride, y, ctl);
 }
 
+static std::atomic<unsigned> g_trsv_spin_limit{1u << 20};
+static std::atomic<int> g_trsv_delay_ticket{-1};
+void set_trsv_spin_limit(unsigned lim) { g_trsv_spin_limit.store(lim ? lim : (1u << 20)); }
+void set_trsv_publish_delay(int ticket) { g_trsv_delay_ticket.store(ticket); }
+
 // L^T x = b (b read with stride bstride, e.g. the bordered row of a Cholesky factor); ctl: 2 words
 void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
-                  double* x, unsigned* ctl, double* xinv_ws) {
+                  double* x, unsigned* ctl, double* xinv_ws, unsigned* err) {
   if (n <= 0) return;
   hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned), st);
   // without the inverse workspace (or IPM_TRSV64=1): the 64-row substitution kernel
   static const bool k64 = [] { const char* e = getenv("IPM_TRSV64"); return e && e[0] == '1'; }();
-  if (k64 || !xinv_ws) {
+  if (k64 || !xinv_ws || !err) {
     trsv_chain(st, false, n, L, ldl, b, bstride, x, ctl);
     return;
   }
@@ -2343,7 +2363,9 @@ void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const
   hipLaunchKernelGGL(k_trinv128, dim3(nblk), dim3(512), 0, st, n, L, ldl, xinv_ws);
   const int grid = std::min(nblk, 256);
   hipMemsetAsync(x, 0xFF, n * sizeof(double), st);   // TRSV_PENDING in every row
-  hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl);
+  hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl,
+                     err, g_trsv_spin_limit.load(std::memory_order_relaxed),
+                     g_trsv_delay_ticket.load(std::memory_order_relaxed));
 }
 
 // Bordered right-hand side: row N of the (N+1) x (N+1) column-major lower factor input holds
@@ -2361,12 +2383,12 @@ void border_rhs(hipStream_t st, int64_t N, double* H, int64_t ldh, const double*
 // L L^T X = B in place; W: scratch n x nrhs (ldb); ctl: device scratch of 4 words (single
 // right-hand side only; may be null, then the blocked multi-RHS path is used)
 void potrs_lower(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws) {
+                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws, unsigned* err) {
   if (n <= 0 || nrhs <= 0) return;
   if (nrhs == 1 && ldb == 1 && ctl) {
     hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned), st);
     trsv_chain(st, true, n, L, ldl, B, 1, W, ctl);
-    trsv_lower_t(st, n, L, ldl, W, 1, B, ctl + 2, xinv_ws);
+    trsv_lower_t(st, n, L, ldl, W, 1, B, ctl + 2, xinv_ws, err);
     return;
   }
   trsm_lower_fwd(st, n, nrhs, L, ldl, B, ldb, W);

@@ -137,17 +137,25 @@ void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H,
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,
-                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws = nullptr);
+                 int64_t ldb, double* W, unsigned* ctl, double* xinv_ws = nullptr, unsigned* err = nullptr);
 // L L^T X = B for many right-hand sides (nrhs >~ 32): 128-row blocks on MFMA GEMMs; ws of
 // potrs_blocked_ws_doubles(n, nrhs) doubles
 int64_t potrs_blocked_ws_doubles(int64_t n, int64_t nrhs);
 void potrs_blocked(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B, int64_t ldb,
                    double* ws);
 // L^T x = b, one right-hand side read with stride bstride; ctl: 2 device words
-// xinv_ws: trsv_inv_ws_doubles(n) doubles for the inverted 128 x 128 diagonal blocks (null: the
-// 64-row substitution kernel)
+// xinv_ws: trsv_inv_ws_doubles(n) doubles for the inverted 128 x 128 diagonal blocks; err: sticky
+// device error word (bit 0: a chain producer missed the spin bound; the caller must read it before
+// using x).  Either null: the 64-row substitution kernel (unbounded waits, no error word).
+// b must not contain the all-ones NaN bit pattern (the persistent solve's "pending" marker).
 void trsv_lower_t(hipStream_t s, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
-                  double* x, unsigned* ctl, double* xinv_ws = nullptr);
+                  double* x, unsigned* ctl, double* xinv_ws = nullptr, unsigned* err = nullptr);
+// spin bound (sleeps) of the backward solve's chain poll; 0 restores the default 2^20 (debug knob:
+// ipm_debug_set_trsv_spin_limit)
+void set_trsv_spin_limit(unsigned lim);
+// debug knob: the workgroup holding this ticket of the backward solve sleeps ~7 ms before it
+// publishes its progress word (-1: none)
+void set_trsv_publish_delay(int ticket);
 inline int64_t trsv_inv_ws_doubles(int64_t n) { return ((n + 127) / 128) * 128 * 128; }
 // H[j*ldh + N] = scale * g[j] (j < N), H[N*ldh + N] = 1e300: bordered right-hand side (see ipm_blas.hip)
 void border_rhs(hipStream_t s, int64_t N, double* H, int64_t ldh, const double* g, double scale);

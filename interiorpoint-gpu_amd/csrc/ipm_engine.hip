@@ -34,6 +34,7 @@ constexpr double STEP_FLOOR = 1e-13;  // NewtonSolver.py:176, 190
 constexpr int NCAND = 64;
 // readback block layout (bytes): info (8 ints), mask (4 words), sums (NCAND), scal (64)
 constexpr int RB_MASK = 32, RB_SUMS = 64, RB_SCAL = RB_SUMS + NCAND * 8;
+constexpr int RB_INFO_TRSV_ERR = 4;   // info word 4: sticky device error word of the backward solve
 constexpr int HOST_WORDS = IPM_HOST_WORDS;
 
 enum Slot {
@@ -237,6 +238,7 @@ int64_t carve(ipm_problem* pr, char* base) {
 }
 
 inline hipStream_t S(ipm_problem* pr) { return pr->h->stream; }
+inline unsigned* trsv_err(ipm_problem* pr) { return reinterpret_cast<unsigned*>(pr->info + RB_INFO_TRSV_ERR); }
 
 // --------------------------------------------------------------- oracle pieces (L1)
 // slack state (s, lhs, rhs) at point xp   (FunctionManager.py:118-149, 427-449, 933-994, 1258-1262)
@@ -562,8 +564,20 @@ extern "C" int ipm_potrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* L
   const int64_t wn = (std::max<int64_t>(n * ldb, 1) + 31) & ~int64_t(31);
   double* W = scratch(h, (wn + trsv_inv_ws_doubles(n)) * sizeof(double));
   if (!W) return IPM_HIP_ERROR;
-  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W, h->ctl, W + wn);
+  unsigned* err = h->ctl + 7;   // potrs_lower uses ctl[0..3]
+  HIPCHK(h, hipMemsetAsync(err, 0, sizeof(unsigned), h->stream));
+  potrs_lower(h->stream, n, nrhs, L, ldl, B, ldb, W, h->ctl, W + wn, err);
   HIPCHK(h, hipGetLastError());
+  if (nrhs == 1 && ldb == 1) {
+    HIPCHK(h, hipMemcpyAsync(h->hbuf, err, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    unsigned e;
+    std::memcpy(&e, h->hbuf, sizeof(unsigned));
+    if (e) {
+      h->err = "backward solve: a chain producer did not publish within the spin bound";
+      return IPM_HIP_ERROR;
+    }
+  }
   return IPM_OK;
 }
 
@@ -640,6 +654,57 @@ extern "C" int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred)
   return IPM_OK;
 }
 
+// HIP-event time (ms, average over reps, on the handle's stream) of the HBM-bound kernels of one
+// Newton step on this problem's own buffers: [0] the slack GEMV C x (k_gemv_n), [1] the gradient
+// GEMV C^T w (k_gemv_t_part + its fold), [2] one 64-candidate line-search pass over the slacks
+// (k_ls_lin).  Clobbers only scratch (Cx, part, pmask/psum).  LP/QP problems with C only.
+extern "C" int ipm_time_hbm_kernels(ipm_problem* pr, int reps, double* ms) {
+  if (!pr || reps <= 0 || !ms || pr->socp || pr->m <= 0) return IPM_INVALID_ARG;
+  ipm_handle* h = pr->h;
+  hipStream_t st = h->stream;
+  const ipm_problem_desc& d = pr->d;
+  hipEvent_t e0, e1;
+  HIPCHK(h, hipEventCreate(&e0));
+  HIPCHK(h, hipEventCreate(&e1));
+  for (int k = 0; k < 3; ++k) {
+    auto launch = [&]() {
+      if (k == 0) gemv_n(st, pr->m, pr->n, 1.0, d.C, d.ldc, pr->xe, 0.0, pr->Cx);
+      else if (k == 1) gemv_t(st, pr->m, pr->n, 1.0, d.C, d.ldc, pr->w, nullptr, 0.0, pr->tmpn, pr->part, pr->part_elems);
+      else ls_lin(st, pr->S, pr->Sbar, pr->s0, pr->ds, 1.0, 0.5, pr->pmask, pr->psum);
+    };
+    launch();   // warm
+    hipEventRecord(e0, st);
+    for (int r = 0; r < reps; ++r) launch();
+    hipEventRecord(e1, st);
+    HIPCHK(h, hipEventSynchronize(e1));
+    float t = 0.f;
+    hipEventElapsedTime(&t, e0, e1);
+    ms[k] = (double)t / reps;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return IPM_OK;
+}
+
+// sizes the HBM-kernel byte counts need: m, n, S (slacks incl. bounds)
+extern "C" int ipm_problem_sizes(ipm_problem* pr, int64_t* out) {
+  if (!pr || !out) return IPM_INVALID_ARG;
+  out[0] = pr->m;
+  out[1] = pr->n;
+  out[2] = pr->S;
+  return IPM_OK;
+}
+
+extern "C" int ipm_debug_set_trsv_spin_limit(unsigned limit) {
+  set_trsv_spin_limit(limit);
+  return IPM_OK;
+}
+
+extern "C" int ipm_debug_set_trsv_publish_delay(int ticket) {
+  set_trsv_publish_delay(ticket);
+  return IPM_OK;
+}
+
 extern "C" int ipm_set_timing(ipm_handle* h, int on) {
   if (!h) return IPM_INVALID_ARG;
   h->timing = on != 0;
@@ -683,6 +748,7 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
     return IPM_INVALID_ARG;
   }
   carve(pr, reinterpret_cast<char*>(workspace));
+  hipMemsetAsync(pr->info, 0, RB_MASK, h->stream);   // info words incl. the sticky device error word
   pr->use_backup = d.solve_method == IPM_SOLVE_LU || d.solve_method == IPM_SOLVE_LSTSQ;
   if (!pr->defer_d.empty() && (d.ldc & 1) == 0 && (((uintptr_t)d.C) & 15) == 0) {
     // deferred KKT slices: the up-front K extent per block, uploaded once
@@ -901,6 +967,15 @@ int readback(ipm_problem* pr, Readback& r, bool want_info) {
   }
   std::memcpy(&r.info, hb, sizeof(int));
   std::memcpy(&r.info2, hb + 4, sizeof(int));
+  int derr;
+  std::memcpy(&derr, hb + 4 * RB_INFO_TRSV_ERR, sizeof(int));
+  if (derr) {
+    // a backward-solve chain producer missed the spin bound: the step in dx is not a solve result
+    hipMemsetAsync(trsv_err(pr), 0, sizeof(unsigned), st);
+    h->err = "backward solve: a chain producer did not publish within the spin bound (device error word " +
+             std::to_string(derr) + "); the Newton step was discarded";
+    return IPM_HIP_ERROR;
+  }
   if (!want_info) r.info = r.info2 = 0;
   std::memcpy(&r.mask, hb + RB_MASK, 8);
   std::memcpy(r.sums, hb + RB_SUMS, NCAND * 8);
@@ -986,7 +1061,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
     potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
     if (h->timing) hipEventRecord(h->ev[3], st);
-    trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv);
+    trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv, trsv_err(pr));
   } else if (!pr->lu) {
     // np_lstsq, and the Cholesky-failure backup (NewtonSolver.py:212-227, 334-341):
     // lstsq(H, -g, rcond=None), minimum norm on the eigenvectors of H
@@ -1123,7 +1198,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
       potrs_lower(st, n, p, pr->H, pr->ldh, pr->Ybuf, p, pr->W2, pr->ctl);
     }
     copy(st, pr->tmpn, pr->g, n);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl, pr->xinv);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl, pr->xinv, trsv_err(pr));
     // S = A Y (lower)
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
@@ -1135,7 +1210,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     // dx = -H^-1 (g + A^T w)
     gemv_t(st, p, n, 1.0, d.A, d.lda, pr->wv, nullptr, 0.0, pr->ATdv, pr->part, pr->part_elems);
     lincomb(st, n, -1.0, pr->g, -1.0, pr->ATdv, pr->dx);
-    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl, pr->xinv);
+    potrs_lower(st, n, 1, pr->H, pr->ldh, pr->dx, 1, pr->W2, pr->ctl, pr->xinv, trsv_err(pr));
     lincomb(st, p, 1.0, pr->wv, -1.0, v, pr->dv);
     return IPM_OK;
   }

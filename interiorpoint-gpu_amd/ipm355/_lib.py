@@ -89,7 +89,11 @@ EXPORTS = {
     "ipm_lstsq_sym": (C.c_int, [P, I64, I64, P, I64, P, I64, C.POINTER(C.c_int)]),
     "ipm_last_timings": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64), C.POINTER(F64)]),
     "ipm_kkt_flops": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
+    "ipm_time_hbm_kernels": (C.c_int, [P, C.c_int, C.POINTER(F64)]),
+    "ipm_problem_sizes": (C.c_int, [P, C.POINTER(I64)]),
     "ipm_set_timing": (C.c_int, [P, C.c_int]),
+    "ipm_debug_set_trsv_spin_limit": (C.c_int, [C.c_uint]),
+    "ipm_debug_set_trsv_publish_delay": (C.c_int, [C.c_int]),
     # batched ADMM Lasso (ipm_lasso.hip; ipm355/lasso.py)
     "ipm_gemm_tn": (C.c_int, [P, I64, I64, I64, F64, P, I64, P, I64, F64, P, I64]),
     "ipm_transpose": (C.c_int, [P, I64, I64, P, I64, P, I64]),

@@ -210,6 +210,18 @@ class DeviceProblem:
         self.call(self.handle.lib.ipm_kkt_flops, self.ptr, ct.byref(a), ct.byref(b))
         return a.value, b.value
 
+    def time_hbm_kernels(self, reps=20):
+        """HIP-event times (ms) of the slack GEMV, the gradient GEMV and one line-search candidate
+        pass on this problem's buffers, with their algorithmic HBM bytes -> {kernel: (ms, bytes)}"""
+        ms = (ct.c_double * 3)()
+        sz = (ct.c_int64 * 3)()
+        self.call(self.handle.lib.ipm_problem_sizes, self.ptr, sz)
+        self.call(self.handle.lib.ipm_time_hbm_kernels, self.ptr, int(reps), ms)
+        m, n, S = int(sz[0]), int(sz[1]), int(sz[2])
+        return {"k_gemv_n (slacks: C x)": (ms[0], 8.0 * (m * n + n + m)),
+                "k_gemv_t_part (gradient: C^T w)": (ms[1], 8.0 * (m * n + m + n)),
+                "k_ls_lin (64 line-search candidates)": (ms[2], 16.0 * S)}
+
     @property
     def use_backup(self):
         return bool(self.handle.lib.ipm_get_use_backup(self.ptr))

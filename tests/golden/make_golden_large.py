@@ -15,6 +15,13 @@ never the inputs themselves (P alone is 512 MiB at n=8192)):
 * ``m3_qp_feas``     the same instance started at its strictly feasible x_f (phase 1 skipped): the
                      first K barrier-phase Newton steps (tP epilogue, P x GEMVs).
 * ``m3_lp``          M3-LP n=8192, m=2048, seed 0, test_LP kwargs: the first K Newton steps.
+* ``m3_qp_full``     the M3-QP headline instance solved to COMPLETION (phase 1 + barrier phase,
+                     QPSolver.py:500-638): x*, value, inner / phase-1 iteration lists, the whole step
+                     trace, x snapshots at steps 10 and 30 (bench.py's rank-0 evidence); envelope = one
+                     1e-15 rhs-perturbed re-run (a 1-thread re-run would take ~6 h here).
+* ``m3_lp_full``     the M3-LP instance solved to completion, same envelope.
+
+Every case also stores ``x_snap_<k>``: the iterate handed to the (k+1)-th line search, k in SNAPS.
 
 Recorded per accepted Newton step: the returned backtracking step size and the Newton decrement
 nd = -g.dx/2 (both exactly what NewtonSolver.solve computes, NewtonSolver.py:93-133); for the
@@ -48,6 +55,7 @@ from QPSolver import QPSolver as RefQP  # noqa: E402
 from ipm355 import problems  # noqa: E402
 
 K_TRUNC = int(os.environ.get("IPM_GOLDEN_K", "30"))
+SNAPS = (10, 30)
 ALT_THREADS = int(os.environ.get("IPM_GOLDEN_ALT_THREADS", "1"))
 
 
@@ -60,6 +68,7 @@ class _Rec:
         self.limit = None
         self.steps, self.nds, self.ph1 = [], [], []
         self.x_at_limit = None
+        self.snaps = {}
 
     def reset(self, limit=None):
         self.__init__()
@@ -73,6 +82,8 @@ def _wrap():
     orig = RNS.NewtonSolver.backtrack_search
 
     def rec(self, x, xstep, t, gradf):
+        if len(REC.steps) in SNAPS:
+            REC.snaps[len(REC.steps)] = np.array(x, copy=True)
         if REC.limit is not None and len(REC.steps) >= REC.limit:
             REC.x_at_limit = np.array(x, copy=True)
             raise _StopK()
@@ -91,7 +102,7 @@ def build(case):
         spec = dict(gen="qp_ineq_box", n=2048, m=512, seed=seed, grid=True)
         inst = problems.qp_ineq_box(2048, 512, seed=seed, grid=True)
         return RefQP, dict(inst, **problems.QP_KWARGS), spec, None
-    if case in ("m3_qp_ph1", "m3_qp_feas"):
+    if case in ("m3_qp_ph1", "m3_qp_feas", "m3_qp_full"):
         spec = dict(gen="qp_ineq_box", n=8192, m=2048, seed=0, grid=True)
         inst = problems.qp_ineq_box(8192, 2048, seed=0, grid=True, with_xf=True)
         xf = inst.pop("xf")
@@ -99,11 +110,11 @@ def build(case):
         if case == "m3_qp_feas":
             kw["x0"] = xf.copy()
             spec["x0"] = "xf"
-        return RefQP, kw, spec, K_TRUNC
-    if case == "m3_lp":
+        return RefQP, kw, spec, (None if case == "m3_qp_full" else K_TRUNC)
+    if case in ("m3_lp", "m3_lp_full"):
         spec = dict(gen="lp_ineq_box", n=8192, m=2048, seed=0, grid=True)
         inst = problems.lp_ineq_box(8192, 2048, seed=0, grid=True)
-        return RefLP, dict(inst, **problems.LP_KWARGS), spec, K_TRUNC
+        return RefLP, dict(inst, **problems.LP_KWARGS), spec, (None if case == "m3_lp_full" else K_TRUNC)
     raise KeyError(case)
 
 
@@ -126,7 +137,7 @@ def run_once(cls, kw, limit):
     ph = getattr(s, "phase1_solver", None)
     return dict(solver=s, x_init=x_init, value=val, xstar=xstar, steps=list(REC.steps), nds=list(REC.nds),
                 ph1=list(REC.ph1), x_limit=REC.x_at_limit,
-                inner_iters=list(getattr(s, "inner_iters", [])),
+                snaps=dict(REC.snaps), inner_iters=list(getattr(s, "inner_iters", [])),
                 phase1_inner_iters=list(getattr(ph, "inner_iters", []) if ph is not None else []))
 
 
@@ -141,6 +152,8 @@ def make(case):
         "trace_phase1": np.array(base["ph1"]), "kwargs": np.array(repr({k: v for k, v in kw.items()
                                                                           if not isinstance(v, np.ndarray)})),
         "ref_seconds": np.array(el)}
+    for k, xs in base["snaps"].items():
+        out[f"x_snap_{k}"] = xs
     if limit is None:
         out.update(value=np.array(base["value"]), xstar=base["xstar"], inner_iters=np.array(base["inner_iters"]),
                    phase1_inner_iters=np.array(base["phase1_inner_iters"]))
@@ -151,7 +164,8 @@ def make(case):
     rng = np.random.default_rng(1234)
     wx, wv, stable, wk = 0.0, 0.0, True, 0.0
     wnd = np.zeros(len(base["nds"]))
-    for _ in range(1 if (limit is not None or case.startswith("m4_")) else 2):
+    big_full = case.endswith("_full")
+    for _ in range(1 if (limit is not None or case.startswith("m4_") or big_full) else 2):
         kp = dict(kw)
         kp[key] = kw[key] * (1 + 1e-15 * rng.standard_normal(kw[key].shape))
         r = run_once(cls, kp, limit)
@@ -168,19 +182,23 @@ def make(case):
     # at 1 OpenBLAS thread (dpotrf's blocking depends on the thread count; a GPU factorization is
     # just another summation order, so this is the envelope the Newton decrements are held to)
     from threadpoolctl import threadpool_limits
-    with threadpool_limits(limits=ALT_THREADS, user_api="blas"):
-        r = run_once(cls, kw, limit)
-    stable &= r["steps"] == base["steps"]
-    if len(r["nds"]) == len(base["nds"]):
-        b = np.array(base["nds"])
-        wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))
-    if limit is None:
-        wx = max(wx, float(np.linalg.norm(r["xstar"] - base["xstar"]) / np.linalg.norm(base["xstar"])))
-        wv = max(wv, abs(r["value"] - base["value"]) / max(abs(base["value"]), 1e-300))
-    elif r["x_limit"] is not None and base["x_limit"] is not None and r["x_limit"].shape == base["x_limit"].shape:
-        wk = max(wk, float(np.linalg.norm(r["x_limit"] - base["x_limit"]) / np.linalg.norm(base["x_limit"])))
-    out.update(sens_sources=np.array(f"{key} * (1 + 1e-15 N(0,1)); OpenBLAS {ALT_THREADS} thread(s) vs "
-                                     f"{os.environ['OPENBLAS_NUM_THREADS']}"))
+    if not big_full:
+        with threadpool_limits(limits=ALT_THREADS, user_api="blas"):
+            r = run_once(cls, kw, limit)
+        stable &= r["steps"] == base["steps"]
+        if len(r["nds"]) == len(base["nds"]):
+            b = np.array(base["nds"])
+            wnd = np.maximum(wnd, np.abs(np.array(r["nds"]) - b) / np.maximum(np.abs(b), 1e-300))
+        if limit is None:
+            wx = max(wx, float(np.linalg.norm(r["xstar"] - base["xstar"]) / np.linalg.norm(base["xstar"])))
+            wv = max(wv, abs(r["value"] - base["value"]) / max(abs(base["value"]), 1e-300))
+        elif r["x_limit"] is not None and base["x_limit"] is not None and r["x_limit"].shape == base["x_limit"].shape:
+            wk = max(wk, float(np.linalg.norm(r["x_limit"] - base["x_limit"]) / np.linalg.norm(base["x_limit"])))
+    else:   # the perturbed run's iteration lists, for the chaotic-envelope report
+        out.update(pert_inner_iters=np.array(r["inner_iters"]), pert_phase1_inner_iters=np.array(r["phase1_inner_iters"]),
+                   pert_trace_step=np.array(r["steps"]))
+    out.update(sens_sources=np.array(f"{key} * (1 + 1e-15 N(0,1))" + ("" if big_full else
+                                     f"; OpenBLAS {ALT_THREADS} thread(s) vs {os.environ['OPENBLAS_NUM_THREADS']}")))
     out.update(sens_key=np.array(key), sens_xstar_rel=np.array(wx), sens_value_rel=np.array(wv),
                sens_xk_rel=np.array(wk), sens_steps_stable=np.array(stable), sens_nd_rel=wnd)
     np.savez_compressed(os.path.join(HERE, case + ".npz"), **out)

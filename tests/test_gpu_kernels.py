@@ -262,3 +262,58 @@ def test_potrs_many_rhs_blocked(n, nrhs):
     err = ((X - ref).abs().max() / ref.abs().max()).item()
     print(f"n={n} nrhs={nrhs}: max rel {err:.2e}")
     assert err < 1e-10
+
+
+def test_trsv_backward_solve_fails_loudly():
+    """The persistent backward solve (k_trsv_bwd128) polls x_{B+1} with a bounded spin.  With the
+    bound shrunk to one sleep (debug knob), a consumer overtakes its producer: the device error
+    word must surface as IPMBackendError, never as a silently wrong step (VERDICT r2 #4)."""
+    from ipm355 import _lib as L
+    h = handle()
+    n = 8192
+    rng = np.random.default_rng(5)
+    M = rng.normal(size=(n + 8, n)) * 2.0 ** -4
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 0 and info == 0
+    b = rng.normal(size=n)
+    ref = np.linalg.solve(A, b)
+    tripped = 0
+    try:
+        h.lib.ipm_debug_set_trsv_spin_limit(1)
+        for _ in range(4):
+            try:
+                potrs(Hm, n, n, b.copy())
+            except L.IPMBackendError as e:
+                assert "spin bound" in str(e)
+                tripped += 1
+    finally:
+        h.lib.ipm_debug_set_trsv_spin_limit(0)
+    assert tripped >= 1
+    x = potrs(Hm, n, n, b.copy()).ravel()    # default bound again: correct, and no sticky error left
+    np.testing.assert_allclose(x, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("ticket", [0, 1, 5])
+def test_trsv_backward_solve_late_publisher(ticket):
+    """A backward-solve workgroup that publishes its progress word late (debug knob: ~7 ms sleep
+    before the store) is overtaken by the next tickets, which read its x block straight from y.
+    The progress word is published with an atomic max, so it never moves backwards and the
+    waiting workgroups still drain (ADVICE r2, high).  Result identical to the undelayed solve."""
+    h = handle()
+    n = 4096
+    rng = np.random.default_rng(11)
+    M = rng.normal(size=(n + 8, n)) * 2.0 ** -4
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 0 and info == 0
+    b = rng.normal(size=n)
+    x0 = potrs(Hm, n, n, b.copy()).ravel()
+    try:
+        h.lib.ipm_debug_set_trsv_publish_delay(ticket)
+        x1 = potrs(Hm, n, n, b.copy()).ravel()
+    finally:
+        h.lib.ipm_debug_set_trsv_publish_delay(-1)
+    np.testing.assert_array_equal(x0, x1)

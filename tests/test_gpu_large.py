@@ -197,6 +197,85 @@ def test_m4_shard_on_one_gpu():
             assert int(tab[i, 1]) == ref_iters
 
 
+def test_sharded_two_ranks_real_solvers(tmp_path):
+    """The sharded driver in TWO processes with the real device solver: launch_local
+    starts 2 ranks (gloo: both share this box's GPU), each runs solve_sharded with QPSolver on its
+    round-robin half of the eight M4 reference fixtures, and the all_gathered table and x* of every
+    instance must match the fixtures on BOTH ranks (the same bars as the one-process shard test)."""
+    import sys
+    from ipm355 import dist
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
+    rc = dist.launch_local(2, [sys.executable, "-u", worker, str(tmp_path)])
+    assert rc == 0
+    zs = [_fixture(f"m4_qp_{sd}") for sd in range(1000, 1008)]
+    for r in range(2):
+        tab = np.load(tmp_path / f"tab{r}.npy")
+        X = np.load(tmp_path / f"x{r}.npy")
+        for i, z in enumerate(zs):
+            err = rel(X[i], z["xstar"])
+            ref_iters = int(sum(z["inner_iters"]) + sum(z["phase1_inner_iters"]))
+            if r == 0:
+                print(f"[rank-gathered m4_qp_{1000 + i}, solved by rank {i % 2}] x* rel {err:.2e}, "
+                      f"iters {int(tab[i, 1])} vs {ref_iters}")
+            assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"])), (r, i, err)
+            assert abs(tab[i, 0] - float(z["value"])) <= \
+                max(1e-8, 4 * float(z["sens_value_rel"])) * abs(float(z["value"]))
+            if bool(z["sens_steps_stable"]):
+                assert int(tab[i, 1]) == ref_iters
+    np.testing.assert_array_equal(np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy"))
+
+
+@pytest.mark.parametrize("name", ["m3_qp_full", "m3_lp_full"])
+def test_m3_full_solve(name):
+    """The headline instance solved to COMPLETION: M3-QP n=8192, m=2048, test_QP
+    kwargs, phase 1 + barrier phase (QPSolver.py:500-638; testSolver.py:563-582), and M3-LP with
+    test_LP kwargs, against the reference's own full solve: x* within max(1e-6, 4x the reference's
+    1e-15-perturbation spread), the value likewise, and -- where the reference's step sequence is
+    stable under that perturbation -- identical iteration counts and step sizes."""
+    s = _check_full(name)
+    z = _fixture(name)
+    steps, _ = _device_trace(s)
+    ref = z["trace_step"]
+    k = min(len(steps), len(ref))
+    first = int(np.argmax(steps[:k] != ref[:k])) if np.any(steps[:k] != ref[:k]) else k
+    p1 = s.phase1_solver
+    print(f"[{name}] device iters {list(s.inner_iters)} phase 1 {list(p1.inner_iters) if p1 is not None else []}; "
+          f"reference {list(z['inner_iters'])} phase 1 {list(z['phase1_inner_iters'])}; reference perturbed "
+          f"{list(z['pert_inner_iters']) if 'pert_inner_iters' in z else '-'}; first differing step {first} of {k}")
+
+
+def test_m5_socp_full_solve():
+    """M5 solved to completion (3 steps before): SOCPSolver n=4096, 256 cones
+    of 16 rows, SOCP_KWARGS (testSolver.py:924-945), against the oracle's stacked-cone full solve
+    (tests/golden/m5_socp_oracle.npz; the reference itself would need 64 GiB of cone caches here).
+    The oracle's own 1e-15 perturbation envelope sets the x* bar; where it is stable, the inner
+    iteration counts and every step size must be identical."""
+    import ast as _ast
+    import ipm355
+    from ipm355 import problems
+    z = _fixture("m5_socp_oracle")
+    spec = _ast.literal_eval(str(z["spec"]))
+    inst = problems.socp_cones(n=spec["n"], K=spec["K"], mi=spec["mi"], seed=spec["seed"])
+    x0 = inst.pop("x0")
+    dg = problems.input_digest({"A": np.stack(inst["A"]), "b": np.stack(inst["b"]), "c": np.stack(inst["c"]),
+                                "q": inst["q"]})
+    assert dg == str(z["digest"])
+    inst["d"] = [float(v) for v in z["d"]]
+    kw = _ast.literal_eval(str(z["kwargs"]))
+    g = ipm355.SOCPSolver(check_cvxpy=False, suppress_print=True, x0=x0.copy(), **inst, **kw)
+    v = g.solve()
+    err = rel(g.xstar, z["xstar"])
+    gs = np.array([t[0] for t in g.ns.trace])
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    print(f"[m5 full] x* rel {err:.2e} (tol {xtol:.1e}), value {v!r} vs {float(z['value'])!r}, iters "
+          f"{list(g.inner_iters)} vs {list(z['inner_iters'])}, oracle stable {bool(z['sens_steps_stable'])}")
+    assert err <= xtol
+    assert abs(v - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * abs(float(z["value"]))
+    if bool(z["sens_steps_stable"]):
+        assert list(g.inner_iters) == list(z["inner_iters"])
+        np.testing.assert_array_equal(gs, z["trace_step"])
+
+
 def test_m5_socp_against_oracle():
     """M5: SOCPSolver n=4096, K=256 cones of 16 rows, P=I, strictly feasible x0 (phase 1 skipped):
     the first centering step truncated to 3 Newton steps on the device and in the oracle."""
