@@ -431,7 +431,14 @@ struct DiagSmem {
 
 // FUSED: inside the one-launch-per-block factorisation (k_potrf_block): the panel was written by
 // other workgroups of the same launch (sc1 loads), and failures are also recorded in *failw.
-template <bool FUSED = false>
+// V (variants, tools/chol_lab.hip): bit 0 -- the leaf waves wait only for the PREVIOUS leaf's
+// published stores at the end of an iteration (progress J+1 needs block row J: tiles from leaves
+// < J and the diagonal block stored by wave 2 in iteration J+1, never the current leaf's rows);
+// bit 1 -- branch-free LDS loads / stores around the leaf (clamped addresses + selects).
+#ifndef IPM_DIAG_V
+#define IPM_DIAG_V 0
+#endif
+template <bool FUSED = false, int V = 0>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
                                           double* __restrict__ dinv_out, int* __restrict__ info,
                                           double* pubL, unsigned* progress, DiagSmem& sm,
@@ -602,7 +609,8 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         row[c] = sD[db + c * 16 + rr];
-        rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
+        if (V & 2) rowb[c] = sD[bb + c * 16 + rr];   // bb == db for absent tiles: a harmless copy
+        else rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
       }
       int bad = 0;
       double piv = readlane_d(row[0], 0);
@@ -638,7 +646,16 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         }
       }
       if (wv == 0) {
-        if (lane < 16) {
+        if (V & 2) {
+          double mine = dvs[0];
+#pragma unroll
+          for (int c = 1; c < 16; ++c) mine = (lane == c) ? dvs[c] : mine;
+          if (lane < 16) {
+            srinv[J * 16 + lane] = mine;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = (rr >= c) ? row[c] : 0.0;   // column-major
+          }
+        } else if (lane < 16) {
 #pragma unroll
           for (int c = 0; c < 16; ++c)
             if (lane == c) srinv[J * 16 + c] = dvs[c];
@@ -669,7 +686,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       for (int I = J + 1 + (wv - f0); I < 8; I += nf) tile_update_n(I, J + 1, J);
       STAMPAT(80 + 8 * wv + J);
     }
-    if (pubL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pubL) {
+      if ((V & 1) && leafw) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the previous leaf's rows
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     STAMP();
     if (fail) break;
@@ -1171,7 +1191,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     ROLE(pb ? 3 : 1);
     if (pb) wait_words(&b.ctl[CTL_NF], 1, (unsigned)b.nnf);
     else wait_la(0, b.wa - 1);
-    diag_role<true>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
+    diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
     return;
   }
   if (kind == K_ROW) {

@@ -5,7 +5,7 @@ Tolerances: fp64 sums of k products in a different order -> |err| <= 64 eps * su
 import numpy as np
 import pytest
 
-from gpu_util import colmajor_lower, dev, host, potrf, potrs, syrk
+from gpu_util import colmajor_lower, dev, handle, host, potrf, potrs, syrk
 
 pytestmark = pytest.mark.gpu
 EPS = np.finfo(np.float64).eps
