@@ -11,8 +11,9 @@ OBJ_DIR  := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-result -Wno-unused-value -Iinclude -I$(SRC_DIR)
 SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_engine.hip $(SRC_DIR)/ipm_lasso.hip $(SRC_DIR)/ipm_lstsq.hip
-# rocSOLVER (dsyevd) + rocBLAS (dgemm): the least-squares fallback only (ipm_lstsq.hip)
-LIBS     := -L/opt/rocm/lib -lrocsolver -lrocblas -Wl,-rpath,/opt/rocm/lib
+# no vendor math libraries: every kernel is hand-written (the least-squares fallback's
+# eigensolver included, ipm_lstsq.hip)
+LIBS     :=
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
 HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
 

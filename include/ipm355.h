@@ -34,6 +34,8 @@ extern "C" {
 #define IPM_INVALID_ARG 2
 #define IPM_HIP_ERROR 3
 #define IPM_NOT_SUPPORTED 4
+#define IPM_LINALG_NOT_CONVERGED 5 /* the least-squares eigensolver did not converge (numpy: LinAlgError
+                                      "SVD did not converge in Linear Least Squares") */
 
 /* problem kinds (LPSolver.py / QPSolver.py / SOCPSolver.py) */
 #define IPM_KIND_LP 0
@@ -208,7 +210,8 @@ int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* LU, int64_t 
    of the np_lstsq method and of the Cholesky-failure backup (NewtonSolver.py:212-227, 334-341;
    NewtonSolverInfeasibleStart.py:279-316, 692-724).  A full symmetric (column-major, lda), replaced
    by its eigenvectors; eigenvalues |lambda| <= eps * n * max|lambda| are dropped (gelsd's rcond
-   rule).  B row-major n x nrhs (ldb), in place.  *info: the eigensolver's convergence info (0 = ok) */
+   rule).  B row-major n x nrhs (ldb), in place.  *info: the eigensolver's convergence info (0 = ok,
+   1 = the hand-written Jacobi eigensolver did not converge) */
 int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda, double* B, int64_t ldb,
                   int* info);
 /* HIP-event timing of the KKT assembly and of the Cholesky factorisation inside

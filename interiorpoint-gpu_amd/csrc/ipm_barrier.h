@@ -27,7 +27,15 @@ struct ResidView {
   const double* Px;                // P x or null
   const double* Pdx;               // P dx or null
   const double* q;                 // or null
-  const double* B;                 // barrier gradient at the (stale) slacks
+  const double* B;                 // barrier gradient at the (stale) slacks (used when blb, bub, ct all null)
+  // the barrier gradient's pieces at the (stale) slacks, combined with the objective gradient in
+  // the reference's own order (FunctionManager.py:248-263: grad = t c; -= 1/s_lb; += 1/s_ub;
+  // += C^T 1/s; SOCP ct_first :1080-1100): at large t the terms cancel to a residual near the
+  // rounding floor, so the association decides whether the backtracking test passes
+  const double* blb = nullptr;
+  const double* bub = nullptr;
+  const double* ct = nullptr;
+  bool ct_first = false;
   const double* ATv;
   const double* ATdv;
   const double* Axb;

@@ -589,7 +589,9 @@ __global__ __launch_bounds__(256) void k_ls_resid(ResidView v, double alpha0, do
   double vals[64];
   if (e < v.n) {
     const double Px = v.Px ? v.Px[e] : 0.0, Pdx = v.Pdx ? v.Pdx[e] : 0.0, q = v.q ? v.q[e] : 0.0;
-    const double B = v.B[e], atv = v.ATv[e], atdv = v.ATdv[e];
+    const bool pieces = v.blb || v.bub || v.ct;
+    const double B = pieces ? 0.0 : v.B[e], atv = v.ATv[e], atdv = v.ATdv[e];
+    const double blb = v.blb ? v.blb[e] : 0.0, bub = v.bub ? v.bub[e] : 0.0, ct = v.ct ? v.ct[e] : 0.0;
     const double tc = v.c ? v.t * v.c[e] : 0.0;
     double a = alpha0;
 #pragma unroll
@@ -601,7 +603,21 @@ __global__ __launch_bounds__(256) void k_ls_resid(ResidView v, double alpha0, do
         if (v.Pdx) px = Px + a * Pdx;
         go = (px + q) * v.t;
       }
-      const double r = ((go + B) + atv) + a * atdv;
+      double g;
+      if (!pieces) {
+        g = go + B;
+      } else if (v.ct_first) {
+        g = go;
+        if (v.ct) g = g + ct;
+        if (v.blb) g = g - blb;
+        if (v.bub) g = g + bub;
+      } else {
+        g = go;
+        if (v.blb) g = g - blb;
+        if (v.bub) g = g + bub;
+        if (v.ct) g = g + ct;
+      }
+      const double r = (g + atv) + a * atdv;
       vals[k] = r * r;
       a = a * beta;
     }

@@ -374,6 +374,17 @@ __device__ __forceinline__ void fmac_bcast16(double& acc, double xb, double x, i
   }
 }
 
+// lane l of this 16-lane row, broadcast to the row (DPP row_newbcast; l must fold to a constant)
+__device__ __forceinline__ double bcast16(double x, int l) {
+  switch (l) {
+#define IPM_BC(k) case k: return __builtin_amdgcn_update_dpp(0.0, x, 0x150 + k, 0xf, 0xf, false);
+    IPM_BC(0) IPM_BC(1) IPM_BC(2) IPM_BC(3) IPM_BC(4) IPM_BC(5) IPM_BC(6) IPM_BC(7)
+    IPM_BC(8) IPM_BC(9) IPM_BC(10) IPM_BC(11) IPM_BC(12) IPM_BC(13) IPM_BC(14) IPM_BC(15)
+#undef IPM_BC
+  }
+  return 0.0;
+}
+
 #ifdef IPM_STAMPS
 __device__ unsigned long long ipm_stamps[128];
 #define STAMP() do { if (tid == 0) ipm_stamps[nst] = __builtin_amdgcn_s_memtime(); ++nst; } while (0)
@@ -436,7 +447,7 @@ struct DiagSmem {
 // < J and the diagonal block stored by wave 2 in iteration J+1, never the current leaf's rows);
 // bit 1 -- branch-free LDS loads / stores around the leaf (clamped addresses + selects).
 #ifndef IPM_DIAG_V
-#define IPM_DIAG_V 0
+#define IPM_DIAG_V 130   // branch-free leaf LDS traffic + look-ahead tiles off wave 3 (tools/chol_lab.hip: 73.0K -> 66.7K cycles)
 #endif
 template <bool FUSED = false, int V = 0>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
@@ -553,6 +564,59 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
     for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = x0[r] + x1[r];
   };
+  // T_{I_t,K} -= sum_{P < np} L_{I_t,P} L_KP^T for up to 3 tiles I_t of ONE block column K at
+  // once (mask: which t are present): the L_KP operand is shared, each term's loads are issued
+  // before the previous term's MFMAs (two terms in flight), so the LDS latency is paid once per
+  // term for all tiles instead of once per term and tile
+  auto tile_update_multi = [&](const int* It, unsigned mask, int K, int np) {
+    const int o = fk * 16 + fr;
+    dbl4 x[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      x[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+      if (mask & (1u << t)) {
+        const int cb = bidx(It[t], K) * 256 + o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[t][r] = sD[cb + 64 * r];
+      }
+    }
+    double av[4], bv[3][4];
+    auto ld = [&](int P) {
+      const int ab = bidx(K, P) * 256 + o;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) av[s4] = -sD[ab + 64 * s4];
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        if (mask & (1u << t)) {
+          const int bb = bidx(It[t], P) * 256 + o;
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) bv[t][s4] = sD[bb + 64 * s4];
+        }
+    };
+    if (np > 0) ld(0);
+    for (int P = 0; P < np; ++P) {
+      double a2[4], b2[3][4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        a2[s4] = av[s4];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) b2[t][s4] = bv[t][s4];
+      }
+      if (P + 1 < np) ld(P + 1);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          if (mask & (1u << t)) x[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s4], b2[t][s4], x[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (mask & (1u << t)) {
+        const int cb = bidx(It[t], K) * 256 + o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = x[t][r];
+      }
+  };
   // final block column Jc of L11 -> A (lower part of the diagonal tile; i, j < nb); tiles
   // I = Jc + part, Jc + part + parts, ...
   auto write_back = [&](int Jc, int part, int parts) {
@@ -613,9 +677,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         else rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
       }
       int bad = 0;
+      double dvs[16];
+      auto sweep = [&]() {
       double piv = readlane_d(row[0], 0);
       double dv = rsqrt_pivot(piv);
-      double dvs[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         if (!(piv > 0.0) && bad == 0) bad = c + 1;
@@ -630,19 +695,59 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         }
         row[c] *= dv;                      // lane c: piv * dv = L_cc
         rowb[c] *= dv;                     // X[r][c] of the tile below
+        if (V & 16) {
+          // the broadcast as a compiler builtin (v_mov_b64 DPP row_newbcast), shared by both row
+          // sets; plain fmas the scheduler can place
 #pragma unroll
-        for (int c2 = c + 1; c2 < 16; ++c2) {
-          fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
-          fmac_bcast16(rowb[c2], row[c], rowb[c], c2, false);
+          for (int c2 = c + 1; c2 < 16; ++c2) {
+            const double bc = bcast16(row[c], c2);
+            row[c2] = fma(-bc, row[c], row[c2]);
+            rowb[c2] = fma(-bc, rowb[c], rowb[c2]);
+          }
+        } else if (V & 64) {
+          // tile-below rows: the multiplier L[c2][c] read into SGPRs (v_readlane), plain v_fma
+#pragma unroll
+          for (int c2 = c + 1; c2 < 16; ++c2) {
+            fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
+            rowb[c2] = fma(-readlane_d(row[c], c2), rowb[c], rowb[c2]);
+          }
+        } else if (V & 32) {
+          // diag rows: the DPP fmac; tile-below rows: the broadcast once more as a DPP mov + fma
+#pragma unroll
+          for (int c2 = c + 1; c2 < 16; ++c2) {
+            fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
+            rowb[c2] = fma(-bcast16(row[c], c2), rowb[c], rowb[c2]);
+          }
+        } else if (V & 1024) {   // lab timing only: no tile-below rows (wrong factor)
+#pragma unroll
+          for (int c2 = c + 1; c2 < 16; ++c2) fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
+        } else {
+#pragma unroll
+          for (int c2 = c + 1; c2 < 16; ++c2) {
+            fmac_bcast16(row[c2], row[c], row[c], c2, c2 == c + 1);
+            fmac_bcast16(rowb[c2], row[c], rowb[c], c2, false);
+          }
         }
         piv = pivn;
         dv = dvn;
       }
+      };
+      if (V & 8192) {   // lab timing only: the sweep twice (the second one warm), stamp between
+        double row0[16], rowb0[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) { row0[c] = row[c]; rowb0[c] = rowb[c]; }
+        sweep();
+        STAMPAT(16 + J);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) { row[c] = row0[c]; rowb[c] = rowb0[c]; }
+        bad = 0;
+      }
+      sweep();
       if (bval) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           sD[bb + c * 16 + rr] = rowb[c];
-          if (pubL) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);
+          if (pubL && !(V & 4096)) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);   // (4096: lab timing only)
         }
       }
       if (wv == 0) {
@@ -669,7 +774,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       // the other waves, off the chain: wave 3 inverts the PREVIOUS diagonal block for the row
       // part; wave 2 publishes it and writes block column J-1 back to A; the free waves apply
       // terms 0..J-1 to the tiles of block column J+1 (look-ahead)
-      if (wv == 3) {
+      if (wv == 3 && !(V & 8)) {   // (V & 8: lab timing only -- the free waves skip their work)
         tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
                       pubL != nullptr);
         STAMPAT(40 + J);
@@ -681,9 +786,31 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       }
       if (wv >= 2) write_back(J - 1, wv - 2, 2);
       STAMPAT(64 + 8 * wv + J);
-      // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin
-      const int f0 = nbt > 4 ? 2 : 1, nf = 4 - f0;
-      for (int I = J + 1 + (wv - f0); I < 8; I += nf) tile_update_n(I, J + 1, J);
+      // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin.  V & 128: wave 3 (the
+      // inverse, ~3900 cycles) takes no look-ahead tiles -- they go to the other free waves
+      const int f0 = nbt > 4 ? 2 : 1;
+      const int nf = (V & 128) ? 3 - f0 : 4 - f0;
+      if (V & 256) {
+        // greedy list schedule of the look-ahead tiles I = J+1..7 over the free waves, by cost
+        // estimates in cycles (lab stamps): the inverse ~4000 (wave 3), publish + write-back
+        // ~1000 (wave 2), a tile ~400 + 250 J; every wave computes the same schedule
+        int It[6] = {0, 0, 0, 0, 0, 0};
+        int nt = 0;
+        int load[4] = {1 << 30, f0 <= 1 ? 0 : (1 << 30), 1000, 4000};
+        for (int I = J + 1; I < 8; ++I) {
+          int best = 1;
+#pragma unroll
+          for (int w = 2; w < 4; ++w)
+            if (load[w] < load[best]) best = w;
+          load[best] += 400 + 250 * J;
+          if (best == wv) It[nt++] = I;   // at most 7 - J <= 6 tiles
+        }
+        if (!(V & 8))
+          for (int t0 = 0; t0 < nt; t0 += 3)
+            tile_update_multi(It + t0, (1u << std::min(3, nt - t0)) - 1u, J + 1, J);
+      } else if (!(V & 8) && !((V & 128) && wv == 3)) {
+        for (int I = J + 1 + (wv - f0); I < 8; I += nf) tile_update_n(I, J + 1, J);
+      }
       STAMPAT(80 + 8 * wv + J);
     }
     if (pubL) {

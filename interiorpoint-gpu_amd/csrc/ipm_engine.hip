@@ -35,6 +35,7 @@ constexpr int NCAND = 64;
 // readback block layout (bytes): info (8 ints), mask (4 words), sums (NCAND), scal (64)
 constexpr int RB_MASK = 32, RB_SUMS = 64, RB_SCAL = RB_SUMS + NCAND * 8;
 constexpr int RB_INFO_TRSV_ERR = 4;   // info word 4: sticky device error word of the backward solve
+constexpr int RB_INFO_LSQ = 5;        // info word 5: non-convergence of the least-squares eigensolver
 constexpr int HOST_WORDS = IPM_HOST_WORDS;
 
 enum Slot {
@@ -239,6 +240,9 @@ int64_t carve(ipm_problem* pr, char* base) {
 
 inline hipStream_t S(ipm_problem* pr) { return pr->h->stream; }
 inline unsigned* trsv_err(ipm_problem* pr) { return reinterpret_cast<unsigned*>(pr->info + RB_INFO_TRSV_ERR); }
+// the Jacobi eigensolver's info (lstsq_sym_factor) goes to its own word: the Cholesky info words
+// keep meaning "factorization failed" (Q9), and a non-converged eigensolve surfaces at the readback
+inline int* lsq_info(ipm_problem* pr) { return pr->info + RB_INFO_LSQ; }
 
 // --------------------------------------------------------------- oracle pieces (L1)
 // slack state (s, lhs, rhs) at point xp   (FunctionManager.py:118-149, 427-449, 933-994, 1258-1262)
@@ -967,6 +971,13 @@ int readback(ipm_problem* pr, Readback& r, bool want_info) {
   }
   std::memcpy(&r.info, hb, sizeof(int));
   std::memcpy(&r.info2, hb + 4, sizeof(int));
+  int lerr;
+  std::memcpy(&lerr, hb + 4 * RB_INFO_LSQ, sizeof(int));
+  if (lerr) {
+    hipMemsetAsync(lsq_info(pr), 0, sizeof(int), st);
+    h->err = "least squares: the Jacobi eigensolver did not converge (numpy: SVD did not converge in Linear Least Squares)";
+    return IPM_LINALG_NOT_CONVERGED;
+  }
   int derr;
   std::memcpy(&derr, hb + 4 * RB_INFO_TRSV_ERR, sizeof(int));
   if (derr) {
@@ -1070,7 +1081,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     if (rc) return rc;
     double* lw = scratch(pr->h, (size_t)lstsq_ws_doubles(pr->N, 1) * sizeof(double));
     if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
-    if (lstsq_sym_factor(&pr->h->rb, st, pr->N, pr->H, pr->ldh, lw, pr->info) ||
+    if (lstsq_sym_factor(&pr->h->rb, st, pr->N, pr->H, pr->ldh, lw, lsq_info(pr)) ||
         lstsq_sym_apply(&pr->h->rb, st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, lw)) {
       pr->h->err = "least-squares library call failed";
       return IPM_HIP_ERROR;
@@ -1106,7 +1117,7 @@ int direction_infeasible_lstsq(ipm_problem* pr, const double* v) {
   double* lws = lw + wh;
   double* stmp = lws + ws;
   void** rb = &pr->h->rb;
-  bool bad = lstsq_sym_factor(rb, st, n, pr->H, pr->ldh, lw, pr->info) != 0;
+  bool bad = lstsq_sym_factor(rb, st, n, pr->H, pr->ldh, lw, lsq_info(pr)) != 0;
   // Y = H^+ A^T (n x p row-major), hg = H^+ g
   copy(st, pr->Ybuf, d.AT, n * p);
   bad = bad || lstsq_sym_apply(rb, st, n, p, pr->H, pr->ldh, pr->Ybuf, p, lw) != 0;
@@ -1117,7 +1128,7 @@ int direction_infeasible_lstsq(ipm_problem* pr, const double* v) {
   syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
   sym_lower_to_full(st, p, pr->Sbuf, lds, stmp, lds);
   copy(st, pr->Sbuf, stmp, p * lds);
-  bad = bad || lstsq_sym_factor(rb, st, p, pr->Sbuf, lds, lws, pr->info + 1) != 0;
+  bad = bad || lstsq_sym_factor(rb, st, p, pr->Sbuf, lds, lws, lsq_info(pr)) != 0;
   gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
   lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
   bad = bad || lstsq_sym_apply(rb, st, p, 1, pr->Sbuf, lds, pr->wv, 1, lws) != 0;
@@ -1156,7 +1167,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
       if (rc) return rc;
       lw = scratch(pr->h, (size_t)lstsq_ws_doubles(p, 1) * sizeof(double));
       if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
-      if (lstsq_sym_factor(&pr->h->rb, st, p, pr->Sbuf, lds, lw, pr->info)) {
+      if (lstsq_sym_factor(&pr->h->rb, st, p, pr->Sbuf, lds, lw, lsq_info(pr))) {
         pr->h->err = "least-squares library call failed";
         return IPM_HIP_ERROR;
       }
@@ -1512,6 +1523,11 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
         rv.Pdx = (!pr->lp && d.P) ? pr->Pdx : nullptr;
         rv.q = pr->lp ? nullptr : d.q;
         rv.B = pr->gb; rv.ATv = pr->ATv; rv.ATdv = pr->ATdv; rv.Axb = pr->Axb; rv.Adx = pr->Adx;
+        // next_grad in the reference's association (see ResidView): the pieces barrier_at left
+        rv.blb = inv_lb(pr);
+        rv.bub = inv_ub(pr);
+        rv.ct = (pr->m > 0 || pr->socp) ? pr->ct : nullptr;
+        rv.ct_first = pr->socp;
         auto resid_pass = [&](int64_t kk0) -> int {
           tab.build(o->beta, kk0 + NCAND);
           ls_resid(st, rv, tab.alpha[kk0], o->beta, pr->pmask, pr->psum);

@@ -109,8 +109,12 @@ struct alignas(16) MfSmem {
 // LOOP 1: the branch-free slab loop only -- the caller guarantees a full 128-tile, whole K slabs
 // (tile_fast_ok) and 16-byte operands; LOOP 0: the general loop only.  (Both loops in one
 // instantiation made the register allocator spill ~2000 VGPRs.)
+// LAZYC (LOOP 1, C -= X^T Y tiles with at least 16 slabs): the accumulators start at zero and the
+// C tile is read one 16 x 16 MFMA block per slab (two slabs ahead of its add), so the 128 KB C read
+// is spread over the K loop instead of a burst before the first MFMA (all workgroups of a round
+// start together: the burst is bandwidth-bound).  C + sum(products) in another association order.
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false, bool SPLITADD = false,
-          int LOOP = 0>
+          int LOOP = 0, bool LAZYC = false, bool CST = false>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
                                           double* part = nullptr, unsigned* pflag = nullptr, int64_t kb = -1,
                                           int64_t ke = -1) {
@@ -209,7 +213,36 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   for (int u = 0; u < TWJ; ++u)
 #pragma unroll
     for (int v = 0; v < TWI; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
-  if (cinit && SPLIT != 1) {
+  static_assert(!LAZYC || (LOOP == 1 && !FOLD && !WEIGHT ), "lazy C: fast loop, no fold, no weight");
+  // CST (LOOP 1 full tiles, C -= X^T Y): the C tile moves through LDS in two 64-column halves --
+  // each wave instruction reads / writes 4 whole 1 KB tile columns instead of 128-byte pieces
+  // in four columns (the MFMA accumulator layout) -- before the first slab and after the last
+  static_assert(!CST || (LOOP == 1 && !FOLD && !LAZYC && BM_ == 128 && WJ == 2), "staged C: 128-tile fast loop");
+  constexpr int CLD = 144;   // staged column stride (doubles): 2 CLD = 32 (mod 64) dwords
+  double* sCst = &sm.sX[0][0];   // sX, sY contiguous: 4 * BK * LD = 64 * CLD doubles
+  static_assert(!CST || 4 * BK * LD >= 64 * CLD, "staging fits the slab buffers");
+  if (CST && cinit && SPLIT == 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = tid + 256 * q, col = e >> 6, rp = e & 63;
+        const double2 v = *reinterpret_cast<const double2*>(a.C + (J0 + 64 * h + col) * a.ldc + I0 + 2 * rp);
+        *reinterpret_cast<double2*>(&sCst[col * CLD + 2 * rp]) = v;
+      }
+      __syncthreads();
+      if (wj == h) {
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[tj][ti][r] = sCst[(tj * 16 + fk + 4 * r) * CLD + wi * (BM / 2) + ti * 16 + fr];
+      }
+      __syncthreads();
+    }
+  } else if (cinit && SPLIT != 1 && !LAZYC) {
 #pragma unroll
     for (int tj = 0; tj < TWJ; ++tj)
 #pragma unroll
@@ -229,7 +262,74 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   // between the MFMAs (the last loads are clamped to slab nslab-1: a harmless reload).  The weight
   // and the sign are applied when the slab goes to LDS.  tools/gemm_lab.hip (lab2): +6-9 %.
   static_assert(LOOP == 0 || (BM_ == 128 && VEC && WJ == 2), "fast loop: 128-tiles, vector loads");
-  if (LOOP == 1) {
+  if constexpr (LAZYC) {
+    // exactly 16 slabs (K = 256: the Cholesky's trailing tiles; the caller guarantees it), fully
+    // unrolled: accumulator block q = s is read in slab s and added in slab s + 2
+    double fx[PT], fy[PT];
+    auto fload = [&](int64_t s) {
+      const double2* xs = reinterpret_cast<const double2*>(xp + s * xstep);
+      const double2* ys = reinterpret_cast<const double2*>(yp + s * ystep);
+#pragma unroll
+      for (int q = 0; q < PT / 2; ++q) {
+        const double2 u = xs[q], v = ys[q];
+        fx[2 * q] = u.x;
+        fx[2 * q + 1] = u.y;
+        fy[2 * q] = v.x;
+        fy[2 * q + 1] = v.y;
+      }
+    };
+    auto fstore = [&](int buf) {
+#pragma unroll
+      for (int q = 0; q < PT; ++q) {
+        sX[buf][sr * LD + sc + q] = fx[q] * xsg;
+        sY[buf][sr * LD + sc + q] = fy[q];
+      }
+    };
+    auto cload = [&](int q) {
+      const int tj = q / TWI, ti = q % TWI;
+      const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
+      const int64_t j0 = J0 + wj * (BM / WJ) + tj * 16 + fk;
+      dbl4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = a.C[(j0 + 4 * r) * a.ldc + i];
+      return v;
+    };
+    constexpr int NS = 16;
+    static_assert(TWJ * TWI == NS, "one accumulator block per slab");
+    dbl4 cq[NS];
+    fload(0);
+    fstore(0);
+    fload(1);
+    cq[0] = cload(0);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int buf = s & 1;
+      const double* bx = sX[buf];
+      const double* by = sY[buf];
+      fstore(buf ^ 1);
+      fload(s + 2 < NS ? s + 2 : NS - 1);
+      if (s + 1 < NS) cq[s + 1] = cload(s + 1);
+      if (s >= 2) acc[(s - 2) / TWI][(s - 2) % TWI] += cq[s - 2];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double av[TWJ], bv[TWI];
+#pragma unroll
+        for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
+#pragma unroll
+        for (int t = 0; t < TWI; ++t) bv[t] = bx[(kk * 4 + fk) * LD + wi * (BM / 2) + t * 16 + fr];
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    acc[(NS - 2) / TWI][(NS - 2) % TWI] += cq[NS - 2];
+    acc[(NS - 1) / TWI][(NS - 1) % TWI] += cq[NS - 1];
+  } else if (LOOP == 1) {
     double fx[PT], fy[PT];
     double fw = 1.0;
     auto fload = [&](int64_t s) {
@@ -317,6 +417,36 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     if (tid == 0)
       while (__hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(2);
     __syncthreads();
+  }
+  if (CST && cinit && SPLIT == 0) {
+    const bool diag = a.tri && I0 == J0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (wj == h) {
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              sCst[(tj * 16 + fk + 4 * r) * CLD + wi * (BM / 2) + ti * 16 + fr] = acc[tj][ti][r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int e = tid + 256 * q, col = e >> 6, rp = e & 63;
+        const double2 v = *reinterpret_cast<const double2*>(&sCst[col * CLD + 2 * rp]);
+        double* cp = a.C + (J0 + 64 * h + col) * a.ldc + I0 + 2 * rp;
+        const int c = 64 * h + col;   // diagonal tile: rows >= c only
+        if (!diag || 2 * rp >= c) {
+          *reinterpret_cast<double2*>(cp) = v;
+        } else if (2 * rp + 1 == c) {   // the pair straddles the diagonal: the lower element only
+          cp[1] = v.y;
+        }
+      }
+      if (h == 0) __syncthreads();
+    }
+    return;
   }
 #pragma unroll
   for (int tj = 0; tj < TWJ; ++tj)

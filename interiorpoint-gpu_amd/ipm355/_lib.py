@@ -18,6 +18,8 @@ IPM_OK = 0
 IPM_NOT_POSITIVE_DEFINITE = 1
 IPM_INVALID_ARG = 2
 IPM_HIP_ERROR = 3
+IPM_NOT_SUPPORTED = 4
+IPM_LINALG_NOT_CONVERGED = 5
 
 KIND_LP, KIND_QP, KIND_SOCP = 0, 1, 2
 SOLVE_CHOLESKY, SOLVE_DIAGONAL, SOLVE_LU, SOLVE_LSTSQ, SOLVE_DIAGONAL_LSTSQ = 0, 1, 2, 3, 4
@@ -175,6 +177,8 @@ class Handle:
         msg = msg.decode() if msg else ""
         if rc == IPM_NOT_POSITIVE_DEFINITE:
             raise np.linalg.LinAlgError(f"matrix not positive definite ({msg})")
+        if rc == IPM_LINALG_NOT_CONVERGED:
+            raise np.linalg.LinAlgError(f"SVD did not converge in Linear Least Squares ({msg})")
         raise IPMBackendError(f"ipm355 error {rc}: {msg}")
 
 

@@ -391,6 +391,19 @@ class Phase1Barrier(_BarrierBase):
         raise ValueError("Hessian is not diagonal, so inverse hessian cannot be directly computed!!")
 
 
+class _LazyBlocks:
+    """list-like per-cone blocks computed on access (memory-light form of the reference's caches)"""
+
+    def __init__(self, fn, k):
+        self.fn, self.k = fn, k
+
+    def __len__(self):
+        return self.k
+
+    def __getitem__(self, i):
+        return self.fn(i)
+
+
 class SOCPBarrier(_BarrierBase):
     """FunctionManagerSOCP (FunctionManager.py:834-1162).
 
@@ -409,8 +422,17 @@ class SOCPBarrier(_BarrierBase):
         self.lb, self.ub = lb, ub
         self.x = x0
         self.t = t
-        self.AtA = [np.matmul(Ai.T, Ai) if Ai.ndim > 1 else np.diag(Ai ** 2) for Ai in A]
-        self.cct = [np.outer(ci, ci) for ci in c] if c is not None else None
+        # the reference caches A_i^T A_i and c_i c_i^T per cone (2 K n^2 doubles: 64 GiB at the M5
+        # size, FunctionManager.py:870-905); above 2 GiB they are recomputed per Hessian instead --
+        # the same BLAS call on the same operands, so the blocks are bitwise the cached ones
+        nx0 = len(x0) if x0 is not None else A[0].shape[-1]
+        self.lazy = len(A) * nx0 * nx0 * 8 * 2 > (2 << 30)
+        if self.lazy:
+            self.AtA = _LazyBlocks(lambda i: np.matmul(A[i].T, A[i]) if A[i].ndim > 1 else np.diag(A[i] ** 2), len(A))
+            self.cct = _LazyBlocks(lambda i: np.outer(c[i], c[i]), len(c)) if c is not None else None
+        else:
+            self.AtA = [np.matmul(Ai.T, Ai) if Ai.ndim > 1 else np.diag(Ai ** 2) for Ai in A]
+            self.cct = [np.outer(ci, ci) for ci in c] if c is not None else None
         self.bounded = lb is not None or ub is not None
         self.constrained = True
         K = len(A)

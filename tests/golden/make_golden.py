@@ -85,7 +85,7 @@ def _permute_vars(kwargs, perm):
     return out
 
 
-def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
+def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4, base_duals=None):
     """The reference's own numerical envelope: re-runs with one input vector perturbed by 1e-15
     (relative) -- first the right-hand side, then the objective vector (c or q: at large t the
     Newton residual is a cancellation of t c against A^T v) -- and, unless x0 comes from the global
@@ -96,6 +96,7 @@ def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
     keys += [k for k in ("c", "q") if isinstance(kwargs.get(k), np.ndarray) and k not in keys][:1]
     rng = np.random.default_rng(1234)
     wx = wv = 0.0
+    wd = {}                      # the duals' own spread (perturbation re-runs; LPSolver.py:641-646)
     stable = True
 
     def copy_kw(kwargs):
@@ -118,6 +119,18 @@ def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
         wx = max(wx, float(np.linalg.norm(xs - base_x) / np.linalg.norm(base_x)))
         wv = max(wv, float(abs(s.value - base_v) / max(abs(base_v), 1e-300)))
         stable &= list(s.inner_iters) == list(base_iters)
+        if base_duals:
+            for k, b0 in base_duals.items():
+                d = np.array(getattr(s, k), copy=True)
+                if unperm is not None and k == "lam_star":
+                    # slack order [d - C x | ub - x | x - lb] (FunctionManager.py:118-149): the bound
+                    # blocks follow the variable order
+                    mC = np.asarray(kwargs["C"]).shape[0] if kwargs.get("C") is not None else 0
+                    nv = len(unperm)
+                    for blk in range((len(d) - mC) // nv):
+                        seg = d[mC + blk * nv: mC + (blk + 1) * nv].copy()
+                        d[mC + blk * nv + unperm] = seg
+                wd[k] = max(wd.get(k, 0.0), float(np.linalg.norm(d - b0) / max(np.linalg.norm(b0), 1e-300)))
 
     for key in keys:
         for _ in range(trials):
@@ -131,6 +144,8 @@ def sensitivity(cls, kwargs, base_x, base_v, base_iters, rand_seed, trials=4):
             perm = rng.permutation(n)
             rerun(_permute_vars(copy_kw(kwargs), perm), unperm=perm)
         tags.append("perm")
+    if base_duals:
+        sensitivity.duals = wd
     return "+".join(tags), wx, wv, stable
 
 
@@ -171,7 +186,12 @@ def run_solve(name, cls, kwargs, solve_kwargs=None, rand_seed=None):
         if getattr(solver, k, None) is not None:
             out[k] = np.asarray(getattr(solver, k))
     saved_trace = list(TRACE)
-    key, wx, wv, stable = sensitivity(cls, kwargs, np.asarray(solver.xstar), float(val), solver.inner_iters, rand_seed)
+    duals = {k: np.asarray(getattr(solver, k)) for k in ("lam_star", "v_star") if getattr(solver, k, None) is not None}
+    sensitivity.duals = {}
+    key, wx, wv, stable = sensitivity(cls, kwargs, np.asarray(solver.xstar), float(val), solver.inner_iters, rand_seed,
+                                      base_duals=duals or None)
+    for k, w in sensitivity.duals.items():          # sens_lam_star_rel / sens_v_star_rel
+        out[f"sens_{k}_rel"] = np.array(w)
     TRACE[:] = saved_trace
     out["sens_key"] = np.array(key)
     out["sens_xstar_rel"] = np.array(wx)

@@ -46,6 +46,24 @@ def nd_excess(nds, ref, spread=None):
     return float(e.max())
 
 
+def centering_step_spread(spread, z):
+    """The n=8192 full-solve fixtures sample the reference's envelope with ONE perturbed re-run (a
+    second ordering would take hours), so the per-step Newton-decrement spread is a single noisy
+    sample.  In the stuck steps of a centering step at large t (Q1: alpha -> 1e-13, H nearly
+    singular) every step has the same conditioning: each step is held to the largest spread the
+    re-run showed within its own centering step (phase-1 and barrier-phase centering steps alike,
+    in the order NewtonSolver ran them)."""
+    counts = list(z["phase1_inner_iters"]) + list(z["inner_iters"])
+    out = np.array(spread, dtype=float, copy=True)
+    k = 0
+    for c in counts:
+        c = int(c)
+        if c > 0:
+            out[k:k + c] = np.max(out[k:k + c])
+        k += c
+    return out
+
+
 def rel(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
@@ -111,7 +129,10 @@ def _check_full(name):
         assert list(s.phase1_solver.inner_iters if s.phase1_solver is not None else []) == \
             list(z["phase1_inner_iters"])
         np.testing.assert_array_equal(steps, z["trace_step"])
-        ndx = nd_excess(nds, z["trace_nd"], z.get("sens_nd_rel"))
+        spread = z.get("sens_nd_rel")
+        if spread is not None and "pert_trace_step" in z:
+            spread = centering_step_spread(spread, z)
+        ndx = nd_excess(nds, z["trace_nd"], spread)
         assert ndx <= 1.0, ndx
     return s
 

@@ -102,6 +102,8 @@ int main(int argc, char** argv) {
   run(k_lab_diag<1>, "V1 deferred store wait");
   run(k_lab_diag<2>, "V2 branch-free LDS loads/stores");
   run(k_lab_diag<3>, "V3 = V1 + V2");
+  run(k_lab_diag<130>, "V130 = V2 + no look-ahead tiles on wave 3");
+  run(k_lab_diag<131>, "V131 = V130 + deferred store wait");
   run(k_lab_diag<0>, "V0 current (again)");
   return 0;
 }
