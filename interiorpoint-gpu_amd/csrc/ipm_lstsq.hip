@@ -16,8 +16,12 @@
 // ordering visits every pair once per sweep of n-1 rounds -- with the rotation that zeroes A_pq
 // (Golub & Van Loan, sym.schur2), applied two-sided to A (each thread owns a 2 x 2 block of A, so
 // the update is in place) and to the columns of V.  Sweeps repeat until no off-diagonal entry is
-// rotated (|A_pq| <= eps sqrt|A_pp A_qq|, or negligible against eps^2 ||A||_F); Jacobi is
-// accurate to high relative precision.  Small systems (n <= JWG_MAX) run the whole iteration in
+// rotated: |A_pq| <= eps sqrt|A_pp A_qq| (relative), or |A_pq| <= eps ||A||_F / n (absolute:
+// the off-diagonal rest then moves an eigenvalue by at most eps ||A||_F, the backward error of
+// gelsd itself).  The absolute bound is needed on rank-deficient H: in the null-space block
+// A_pp, A_qq and A_pq are all rounding noise of the large rotations, the relative test keeps
+// rotating that noise forever (a numpy restatement at n = 1025, rank 700 never stops), and those
+// eigenvalues fall below gelsd's cut anyway.  Small systems (n <= JWG_MAX) run the whole iteration in
 // ONE workgroup (no launches per round); larger ones one rotation + one update launch per round and
 // a 4-byte readback per sweep.  Non-convergence within JMAX_SWEEPS sets *info_dev = 1 (the host
 // raises LinAlgError like numpy's "SVD did not converge").
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
   __shared__ double sc[JWG_MAX + 1], ss[JWG_MAX + 1];
   __shared__ int srot;
   const int nn = n + (n & 1), half = nn / 2, tid = threadIdx.x;
-  const double tiny = DBL_EPSILON * DBL_EPSILON * sqrt(*frob2);
+  const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
   int sweep = 0;
   for (; sweep < JMAX_SWEEPS; ++sweep) {
     if (tid == 0) srot = 0;
@@ -164,7 +168,7 @@ __global__ void k_jacobi_rot(int n, int r, const double* __restrict__ A, int64_t
   const int nn = n + (n & 1), half = nn / 2;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= half) return;
-  const double tiny = DBL_EPSILON * DBL_EPSILON * sqrt(*frob2);
+  const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
   int a, b;
   circle_pair(nn, r, i, a, b);
   const int p = min(a, b), q = max(a, b);

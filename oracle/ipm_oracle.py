@@ -547,6 +547,48 @@ class SOCPBarrier(_BarrierBase):
             self.update_t(t)
         if not self.dirty_hess:
             return self.hess
+        if self.lazy and all(Ai.ndim > 1 for Ai in self.A):
+            H = self._hessian_stacked()
+        else:
+            H = self._hessian_blocks()
+        if self.bounded:
+            dg = np.einsum("ii->i", H)
+            if self.lb is not None:
+                dg += 1 / (self.slacks[self.seg_lb] + EPS_CONE) ** 2
+            if self.ub is not None:
+                dg += 1 / (self.slacks[self.seg_ub] + EPS_CONE) ** 2
+        self.hess = H
+        self.dirty_hess = False
+        return H
+
+    def _hessian_stacked(self):
+        """The same sum as _hessian_blocks in ONE weighted Gram product (the device's layout,
+        DESIGN.md §3): rows A_i (weight 2/(s_i+eps)), c_i (same weight), g_i (weight 1), so
+        H = tP + X^T diag(w) X.  Used only above the 2 GiB cache size (the M5 fixture,
+        tests/golden/make_golden_m5.py), where the per-cone form streams ~1 GB of n x n temporaries
+        per cone and a Hessian takes minutes; it sums in another order than the reference's
+        per-cone loop (rounding-level differences, covered by the fixture's perturbation envelope)."""
+        rows, wts = [], []
+        for i, (Ai, s) in enumerate(zip(self.A, self.slacks[self.seg_cone])):
+            sc = 2 / (s + EPS_CONE)
+            gt = Ai.T @ self.lhs[i]
+            rows.append(Ai)
+            wts.append(np.full(Ai.shape[0], sc))
+            if self.c is not None:
+                gt -= self.c[i] * self.rhs[i]
+                rows.append(self.c[i][None, :])
+                wts.append(np.array([sc]))
+            gt *= sc
+            rows.append(gt[None, :])
+            wts.append(np.array([1.0]))
+        X = np.concatenate(rows, axis=0)
+        w = np.concatenate(wts)
+        H = X.T @ (w[:, None] * X)
+        if self.P is not None:
+            H += self.t * self.P
+        return H
+
+    def _hessian_blocks(self):
         H = 0
         if self.P is not None:
             H += self.t * self.P
@@ -561,14 +603,6 @@ class SOCPBarrier(_BarrierBase):
             gt *= 2 / (s + EPS_CONE)
             blk += np.outer(gt, gt)
             H += blk
-        if self.bounded:
-            dg = np.einsum("ii->i", H)
-            if self.lb is not None:
-                dg += 1 / (self.slacks[self.seg_lb] + EPS_CONE) ** 2
-            if self.ub is not None:
-                dg += 1 / (self.slacks[self.seg_ub] + EPS_CONE) ** 2
-        self.hess = H
-        self.dirty_hess = False
         return H
 
     def inv_hessian(self, x=None):

@@ -205,6 +205,7 @@ def test_getrf_getrs_match_numpy(n):
 
 
 @pytest.mark.parametrize("n,rank,nrhs,indef", [(50, 50, 1, False), (200, 120, 3, False), (300, 90, 1, True),
+                                               (301, 90, 1, False), (1024, 700, 1, False), (1025, 1025, 1, False),
                                                (1025, 700, 2, False)])
 def test_lstsq_sym_matches_numpy(n, rank, nrhs, indef):
     """Minimum-norm least squares (ipm_lstsq_sym: eigenvectors, gelsd's rcond = eps*n cut) vs
