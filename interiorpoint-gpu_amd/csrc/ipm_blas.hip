@@ -784,7 +784,13 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
         for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
       }
-      if (wv >= 2) write_back(J - 1, wv - 2, 2);
+      // V & 512: wave 2 writes the whole block column back, so that wave 3's store wait (its
+      // vmcnt(0) before the barrier) covers only its Dinv stores
+      if (V & 512) {
+        if (wv == 2) write_back(J - 1, 0, 1);
+      } else if (wv >= 2) {
+        write_back(J - 1, wv - 2, 2);
+      }
       STAMPAT(64 + 8 * wv + J);
       // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin.  V & 128: wave 3 (the
       // inverse, ~3900 cycles) takes no look-ahead tiles -- they go to the other free waves

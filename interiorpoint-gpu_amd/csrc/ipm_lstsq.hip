@@ -62,27 +62,51 @@ __device__ __forceinline__ bool jacobi_rot(double app, double aqq, double apq, d
   return true;
 }
 
-// the 2 x 2 block (rows of pair P, columns of pair Q) of A <- J^T A J, in place
-__device__ __forceinline__ void jacobi_block(double* A, int64_t lda, int p1, int q1, double c1, double s1, int p2,
-                                             int q2, double c2, double s2, bool diag) {
-  double* a11 = A + (int64_t)p2 * lda + p1;   // (p1, p2)
-  double* a12 = A + (int64_t)q2 * lda + p1;   // (p1, q2)
-  double* a21 = A + (int64_t)p2 * lda + q1;   // (q1, p2)
-  double* a22 = A + (int64_t)q2 * lda + q1;   // (q1, q2)
-  const double x11 = *a11, x12 = *a12, x21 = *a21, x22 = *a22;
-  // rows: r_p = c r_p - s r_q, r_q = s r_p + c r_q
-  const double y11 = c1 * x11 - s1 * x21, y12 = c1 * x12 - s1 * x22;
-  const double y21 = s1 * x11 + c1 * x21, y22 = s1 * x12 + c1 * x22;
-  // columns: likewise with the column pair's rotation
-  double z11 = c2 * y11 - s2 * y12, z12 = s2 * y11 + c2 * y12;
-  double z21 = c2 * y21 - s2 * y22, z22 = s2 * y21 + c2 * y22;
-  if (diag) {   // the rotated pair itself: symmetric, off-diagonal zero by construction
-    z12 = z21 = 0.0;
+// pair encoding: p | (q << 16), q = JSINGLE when the pair is an odd n's last index with the dummy
+// player -- a single index p that no rotation touches, but whose entries in the rotated rows and
+// columns of the OTHER pairs still turn with them
+constexpr int JSINGLE = 0xFFFF;
+__device__ __forceinline__ int jpack(int p, int q, int n) { return p | ((q < n ? q : JSINGLE) << 16); }
+
+// the block (rows of pair P, columns of pair Q) of A <- J^T A J, in place: 2 x 2 for two real pairs,
+// 2 x 1 / 1 x 2 when one side is a single index (identity rotation on that side), nothing for two
+// singles
+__device__ __forceinline__ void jacobi_block(double* A, int64_t lda, int pp, double c1, double s1, int pq, double c2,
+                                             double s2, bool diag) {
+  const int p1 = pp & 0xFFFF, q1 = (pp >> 16) & 0xFFFF, p2 = pq & 0xFFFF, q2 = (pq >> 16) & 0xFFFF;
+  const bool r2 = q1 != JSINGLE, k2 = q2 != JSINGLE;
+  if (r2 && k2) {
+    double* a11 = A + (int64_t)p2 * lda + p1;   // (p1, p2)
+    double* a12 = A + (int64_t)q2 * lda + p1;   // (p1, q2)
+    double* a21 = A + (int64_t)p2 * lda + q1;   // (q1, p2)
+    double* a22 = A + (int64_t)q2 * lda + q1;   // (q1, q2)
+    const double x11 = *a11, x12 = *a12, x21 = *a21, x22 = *a22;
+    // rows: r_p = c r_p - s r_q, r_q = s r_p + c r_q
+    const double y11 = c1 * x11 - s1 * x21, y12 = c1 * x12 - s1 * x22;
+    const double y21 = s1 * x11 + c1 * x21, y22 = s1 * x12 + c1 * x22;
+    // columns: likewise with the column pair's rotation
+    double z11 = c2 * y11 - s2 * y12, z12 = s2 * y11 + c2 * y12;
+    double z21 = c2 * y21 - s2 * y22, z22 = s2 * y21 + c2 * y22;
+    if (diag) {   // the rotated pair itself: symmetric, off-diagonal zero by construction
+      z12 = z21 = 0.0;
+    }
+    *a11 = z11;
+    *a12 = z12;
+    *a21 = z21;
+    *a22 = z22;
+  } else if (r2) {   // column p2 alone: rows (p1, q1) turn
+    double* a11 = A + (int64_t)p2 * lda + p1;
+    double* a21 = A + (int64_t)p2 * lda + q1;
+    const double x11 = *a11, x21 = *a21;
+    *a11 = c1 * x11 - s1 * x21;
+    *a21 = s1 * x11 + c1 * x21;
+  } else if (k2) {   // row p1 alone: columns (p2, q2) turn
+    double* a11 = A + (int64_t)p2 * lda + p1;
+    double* a12 = A + (int64_t)q2 * lda + p1;
+    const double x11 = *a11, x12 = *a12;
+    *a11 = c2 * x11 - s2 * x12;
+    *a12 = s2 * x11 + c2 * x12;
   }
-  *a11 = z11;
-  *a12 = z12;
-  *a21 = z21;
-  *a22 = z22;
 }
 
 __device__ __forceinline__ void jacobi_vcols(double* V, int64_t n, int p, int q, double c, double s, int64_t k) {
@@ -135,7 +159,7 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
         double c = 1.0, s = 0.0;
         if (q < n && jacobi_rot(A[(int64_t)p * lda + p], A[(int64_t)q * lda + q], A[(int64_t)q * lda + p], tiny, c, s))
           atomicAdd(&srot, 1);
-        spart[i] = (q < n) ? (p | (q << 16)) : -1;
+        spart[i] = jpack(p, q, n);
         sc[i] = c;
         ss[i] = s;
       }
@@ -144,14 +168,13 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
       for (int e = tid; e < half * half; e += 1024) {
         const int P = e / half, Q = e % half;
         const int pp = spart[P], pq = spart[Q];
-        if (pp < 0 || pq < 0) continue;
         if (sc[P] == 1.0 && ss[P] == 0.0 && sc[Q] == 1.0 && ss[Q] == 0.0) continue;
-        jacobi_block(A, lda, pp & 0xFFFF, pp >> 16, sc[P], ss[P], pq & 0xFFFF, pq >> 16, sc[Q], ss[Q], P == Q);
+        jacobi_block(A, lda, pp, sc[P], ss[P], pq, sc[Q], ss[Q], P == Q);
       }
       for (int e = tid; e < half * n; e += 1024) {
         const int P = e / n, k = e % n;
         const int pp = spart[P];
-        if (pp < 0 || (sc[P] == 1.0 && ss[P] == 0.0)) continue;
+        if (sc[P] == 1.0 && ss[P] == 0.0) continue;   // (singles always: identity)
         jacobi_vcols(V, n, pp & 0xFFFF, pp >> 16, sc[P], ss[P], k);
       }
       __syncthreads();
@@ -175,7 +198,7 @@ __global__ void k_jacobi_rot(int n, int r, const double* __restrict__ A, int64_t
   double c = 1.0, s = 0.0;
   if (q < n && jacobi_rot(A[(int64_t)p * lda + p], A[(int64_t)q * lda + q], A[(int64_t)q * lda + p], tiny, c, s))
     atomicAdd(nrot, 1);
-  part[i] = (q < n) ? (p | (q << 16)) : -1;
+  part[i] = jpack(p, q, n);
   cs[2 * i] = c;
   cs[2 * i + 1] = s;
 }
@@ -188,16 +211,15 @@ __global__ void k_jacobi_upd(int n, double* A, int64_t lda, double* V, const int
   if (e < nA) {
     const int P = (int)(e % half), Q = (int)(e / half);   // consecutive threads: consecutive row pairs
     const int pp = part[P], pq = part[Q];
-    if (pp < 0 || pq < 0) return;
     const double c1 = cs[2 * P], s1 = cs[2 * P + 1], c2 = cs[2 * Q], s2 = cs[2 * Q + 1];
     if (c1 == 1.0 && s1 == 0.0 && c2 == 1.0 && s2 == 0.0) return;
-    jacobi_block(A, lda, pp & 0xFFFF, pp >> 16, c1, s1, pq & 0xFFFF, pq >> 16, c2, s2, P == Q);
+    jacobi_block(A, lda, pp, c1, s1, pq, c2, s2, P == Q);
   } else if (e < nA + (int64_t)half * n) {
     const int64_t f = e - nA;
     const int P = (int)(f / n);
     const int64_t k = f % n;
     const int pp = part[P];
-    if (pp < 0 || (cs[2 * P] == 1.0 && cs[2 * P + 1] == 0.0)) return;
+    if (cs[2 * P] == 1.0 && cs[2 * P + 1] == 0.0) return;   // (singles always: identity)
     jacobi_vcols(V, n, pp & 0xFFFF, pp >> 16, cs[2 * P], cs[2 * P + 1], k);
   }
 }

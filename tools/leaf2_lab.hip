@@ -239,8 +239,8 @@ int main() {
     }
   }
   };
-  stamped(k_stamped<2>, 2);
-  stamped(k_stamped<8192 + 2>, 8194);
+  stamped(k_stamped<130>, 130);
+  stamped(k_stamped<130 + 512>, 642);
 
 
 
@@ -258,10 +258,10 @@ int main() {
     hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
     printf("%-46s %6llu cycles per 16-column sweep (incl. restore)\n", name, c);
   };
-  sweep(k_sweep<0>, "sweep as shipped (diag + tile-below rows)");
+  if (0) sweep(k_sweep<0>, "sweep as shipped (diag + tile-below rows)");
   sweep(k_sweep<1>, "diag rows only");
   sweep(k_sweep<2>, "pivot chain only");
-  sweep(k_sweep<3>, "rank-1 DPP updates only (both row sets)");
+  if (0) sweep(k_sweep<3>, "rank-1 DPP updates only (both row sets)");
   sweep(k_sweep<4>, "restore only");
   auto sweep4 = [&](auto kern, const char* name) {
     hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, 0, io, out, cyc, 200);
