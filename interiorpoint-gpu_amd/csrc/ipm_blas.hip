@@ -1109,7 +1109,19 @@ struct BlockArgs {
   int64_t s_full = 0;
   double* sscr = nullptr;       // split p's upper-half partial tile at sscr + p * 128 * 128
   unsigned* sflag = nullptr;    // split p done: sflag[p]
+  // block pairs (IPM_PAIR, potrf_pair_plan): the trailing tiles apply TWO earlier blocks at once
+  // (K = 512: C read and written once per 512 columns of L instead of per 256).  S tickets
+  // [0, nstrip) are the strip tiles (s2: the next block's 256 columns, 2 tiles per tile row); the
+  // rest index the far-region tile list of s from f0 on (a pair's two launches each take a part).
+  int64_t nstrip = 0, f0 = 0;
+  GemmArgs s2;
+  int rag_K = CH_NB;            // ragged rows: K extent and first column of the applied blocks
+  int64_t rag_cp = 0;
+  int flex = 0;                 // IPM_FLEX: trailing tiles and non-critical row chunks share tickets
 };
+#ifndef FLEX_PROG
+#define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
+#endif
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
   CTL_NF = 9,                         // next-diagonal-block fold tiles done
@@ -1118,7 +1130,8 @@ enum {
   // by a workgroup that landed on that CU
   CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
   CTL_XQ = CTL_SPILL + NCRIT,         // trailing-tile queue counter of each XCD (8 words)
-  CTL_HDR = CTL_XQ + 8
+  CTL_FLEX_S = CTL_XQ + 8, CTL_FLEX_R,  // flexible tickets: trailing tiles / row chunks taken
+  CTL_HDR = CTL_FLEX_R + 1
 };
 
 // Trailing tiles by XCD (s_map 2): the tri tile list is cut into 8 contiguous runs; a workgroup
@@ -1288,6 +1301,47 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       const int64_t na = b.nra - nchd;
       if (t < b.nrag) {
         kind = K_RAG;
+      } else if (b.flex && (t -= b.nrag) < b.ns + na + b.nrb) {
+        // flexible tickets: one item each from two queues -- the remaining row chunks (P(a) ones,
+        // then P(b) ones) once their diagonal role has published FLEX_PROG block rows, else the
+        // next trailing tile.  Every ticket gets exactly one item (tickets = items; a ticket finding
+        // the tile queue exhausted takes a row chunk regardless).  A row chunk then waits only for
+        // its diagonal role, look-ahead tiles (lower tickets) and, for P(b), P(a) chunks that an
+        // earlier flexible ticket took: no cycle.  Row chunks start as their panel is ready instead
+        // of after every trailing tile.
+        __shared__ long long sflex;
+        if (tid == 0) {
+          const unsigned nr = (unsigned)(na + b.nrb), nsv = (unsigned)b.ns;
+          long long item = -1;
+          const unsigned r = ld_ctl(&b.ctl[CTL_FLEX_R]);
+          const bool ready = r < nr && ld_ctl(&b.ctl[r < (unsigned)na ? CTL_PA_PROG : CTL_PB_PROG]) >= (unsigned)FLEX_PROG;
+          if (ready) {
+            const unsigned r2 = atomicAdd(&b.ctl[CTL_FLEX_R], 1u);
+            if (r2 < nr) item = (1ll << 40) | r2;
+          }
+          if (item < 0) {
+            const unsigned s2 = atomicAdd(&b.ctl[CTL_FLEX_S], 1u);
+            if (s2 < nsv) item = s2;
+          }
+          if (item < 0) {
+            const unsigned r2 = atomicAdd(&b.ctl[CTL_FLEX_R], 1u);
+            if (r2 < nr) item = (1ll << 40) | r2;
+          }
+          sflex = item;
+        }
+        __syncthreads();
+        const long long it = sflex;
+        if (it >= (1ll << 40)) {
+          const int64_t r = it & 0xFFFFFFFFll;
+          kind = K_ROW;
+          pb = r >= na;
+          chunk = pb ? r - na : nchd + r;
+        } else if (it >= 0) {
+          kind = K_TILE;
+          t = it;
+        }
+      } else if (b.flex) {
+        if ((t -= b.ns + na + b.nrb) < b.gs_total) kind = K_GS;
       } else if ((t -= b.nrag) < b.ns) {
         kind = K_TILE;
       } else if ((t -= b.ns) < na) {
@@ -1442,12 +1496,12 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     // ragged rows i in [r0, r0 + rn) of the trailing update (origin o, K = the previous block's
     // 256 columns): C(i, j) -= sum_k L(i, k) L(j, k) for j <= i; workgroup t takes columns
     // j = 256 t + tid.  Nothing else in this launch touches these elements.
-    const int64_t o = b.cb + b.wa + b.wbw, cp = b.cb - CH_NB;
+    const int64_t o = b.cb + b.wa + b.wbw, cp = b.rag_cp;
     const int64_t m = b.n - o, r0 = b.rag_r0;
-    const int rn = b.rag_n;
-    double* xr = sm.d.sD;   // xr[q * CH_NB + k] = L(o + r0 + q, cp + k)
-    for (int e = tid; e < rn * CH_NB; e += 256) {
-      const int q = e / CH_NB, k = e - q * CH_NB;
+    const int rn = b.rag_n, KR = b.rag_K;   // KR <= 512: rn * KR <= 4096 doubles of sD
+    double* xr = sm.d.sD;   // xr[q * KR + k] = L(o + r0 + q, cp + k)
+    for (int e = tid; e < rn * KR; e += 256) {
+      const int q = e / KR, k = e - q * KR;
       xr[e] = b.A[(cp + k) * b.lda + o + r0 + q];
     }
     __syncthreads();
@@ -1459,11 +1513,11 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       for (int q = 0; q < 8; ++q) acc[q] = (q < rn && j <= r0 + q) ? cj[q] : 0.0;
       const double* xp = b.A + cp * b.lda + o + j;   // L(o + j, cp + k) = xp[k * lda]
 #pragma unroll 16
-      for (int k = 0; k < CH_NB; ++k) {
+      for (int k = 0; k < KR; ++k) {
         const double xj = xp[k * b.lda];
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-          if (q < rn) acc[q] = fma(-xj, xr[q * CH_NB + k], acc[q]);
+          if (q < rn) acc[q] = fma(-xj, xr[q * KR + k], acc[q]);
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -1503,14 +1557,32 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       const int v = sflag;
       __syncthreads();
       if (v) {
-        // S ticket -> whole tile, or one K-half of a split tile (pieces: upper half, then lower)
-        const int64_t st = v - 1, u = st - b.s_full;
+        // S ticket -> strip tile (pair launches), whole tile, or one K-half of a split tile
+        // (pieces: upper half, then lower)
+        const int64_t st0 = v - 1;
+        const bool strip = st0 < b.nstrip;
+        const int64_t st = strip ? st0 : st0 - b.nstrip, u = strip ? -1 : st - b.s_full;
         const int sp = u < 0 ? 0 : ((u & 1) ? 2 : 1);
         const int64_t p = u < 0 ? 0 : (u >> 1);
+        GemmArgs g = b.s;
+        if (strip) {
+          g.ni = b.s2.ni;
+          g.nj = b.s2.nj;
+          g.X = b.s2.X;
+          g.Y = b.s2.Y;
+          g.C = b.s2.C;
+          g.rowmajor = 1;
+          g.xcd_remap = 0;
+          g.tiles_i = b.s2.tiles_i;
+          g.tiles_j = b.s2.tiles_j;
+          g.nblk = b.s2.nblk;
+        }
         // (both loops in one kernel raised the SGPR spills 89 -> 621 and cost 2.5 %: the launch
         // picks the kernel instead, FASTS)
         mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0>(
-            b.s, u < 0 ? st : b.s_full + p, sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
+            g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
+                     : b.f0 + (u < 0 ? st : b.s_full + p),
+            sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
       }
     }
   }
@@ -1553,13 +1625,16 @@ static double split_makespan(int slots, const std::vector<std::pair<int64_t, dou
     }
   return mk;
 }
+// (pair launches, K = 512: tiles cost tc = 1.6 (tools/tile_lab.hip: 154 vs 96 us), look-ahead
+// tiles twice their K = 256 cost, and the nstrip strip tiles come first)
 static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t ns, int64_t nrows,
-                          int64_t cap) {
+                          int64_t cap, double tc = 1.0, int64_t nstrip = 0, double lac = 0.8) {
   if (ns < 64) return 0;
   const int slots = 2 * num_cus();
   auto mk = [&](int64_t q) {
-    std::vector<std::pair<int64_t, double>> it = {{nla, 0.8}, {1, 0.6}, {nchd, 0.66}, {nnf, 0.8}, {pb ? 1 : 0, 1.25},
-                                                  {nrag, 0.1}, {ns - q, 1.0}, {2 * q, 0.55}, {nrows, 0.5}};
+    std::vector<std::pair<int64_t, double>> it = {{nla, lac}, {1, 0.6}, {nchd, 0.66}, {nnf, 0.8}, {pb ? 1 : 0, 1.25},
+                                                  {nrag, 0.1 * tc}, {nstrip, tc}, {ns - q, tc}, {2 * q, 0.55 * tc},
+                                                  {nrows, 0.5}};
     return split_makespan(slots, it);
   };
   const double m0 = mk(0);
@@ -1570,6 +1645,41 @@ static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64
     if (m < best - 0.02) { best = m; bq = q; }
   }
   return bq;
+}
+
+// ---- block pairs.  Launch kinds: 0 plain (the trailing update of block b-1 over everything right
+// of block b); 2 EVEN e (its look-ahead tiles, the next block's strip and the first f1 tiles of the
+// far region F -- everything right of block e+1 -- apply the PAIR e-2, e-1 with K = 512); 1 ODD
+// e+1 (look-ahead: block e, K = 256; trailing: the rest of F with the pair e-2, e-1).  The launch
+// before the first EVEN is an ODD with nothing to apply (its chain runs without trailing work once);
+// the last EVEN takes all of F and plain launches follow.  Pairs run while F has at least
+// IPM_PAIR_MIN rows (default 3072: trailing-bound launches); IPM_PAIR=0 turns them off.
+struct PairPlan {
+  std::vector<int> kind;      // per 256-column block
+  std::vector<int64_t> f1;    // EVEN: F tiles it takes (tile list [0, f1)); ODD: the EVEN's f1
+};
+static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks, bool defer) {
+  PairPlan pl;
+  pl.kind.assign(nblocks, 0);
+  pl.f1.assign(nblocks, 0);
+  // (off by default: measured 6.49 -> 6.73 ms at n = 8192, r3 pair_ab -- the early pairs gain ~0.4 ms,
+  // the later ones lose more: their K = 512 tiles fill one round and the row chunks queue behind)
+  static const bool on = [] { const char* e = getenv("IPM_PAIR"); return e && e[0] == '1'; }();
+  static const int64_t minrows = [] { const char* e = getenv("IPM_PAIR_MIN"); return e ? atoll(e) : 3072LL; }();
+  if (!on || defer || ncols < n - 8) return pl;   // (a partial factorisation keeps the plain order)
+  // EVEN e needs block e+1 to exist and F = rows beyond block e+1 of at least minrows
+  int64_t last = -1;
+  for (int64_t e = 2; e + 1 < nblocks; e += 2) {
+    if (n - (e + 2) * CH_NB < minrows) break;
+    last = e;
+  }
+  if (last < 0) return pl;
+  pl.kind[1] = 1;                                  // ODD with nothing pending
+  for (int64_t e = 2; e <= last; e += 2) {
+    pl.kind[e] = 2;
+    if (e < last) pl.kind[e + 1] = 1;
+  }
+  return pl;
 }
 
 void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
@@ -1591,7 +1701,10 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   // IPM_SPLIT=0: no K-split trailing tiles (read per call: tests compare both)
   const char* esp = getenv("IPM_SPLIT");
   const bool split_on = !(esp && esp[0] == '0');
+  PairPlan pl = potrf_pair_plan(n, ncols, nblocks, defer);
   for (int64_t bk = 0; bk < nblocks; ++bk) {
+    const int kind = pl.kind[bk];
+    const int64_t Kla = kind == 2 ? 2 * CH_NB : CH_NB;   // look-ahead depth (EVEN: the pair)
     BlockArgs b;
     b.n = n;
     b.lda = lda;
@@ -1606,14 +1719,14 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     b.wa = (int)std::min<int64_t>(wb, PF_NB);
     b.wbw = (int)(wb - b.wa);
     if (bk > 0) {
-      const int64_t cp = cb - CH_NB;
+      const int64_t cp = cb - Kla;
       const int64_t ni = n - cb;
       // rows [0, 128) x columns [0, min(128, wb)), lower: 32-tiles (tri enumeration)
       GemmArgs& c = b.la32;
       c.ni = std::min<int64_t>(ni, 128);
       c.nj = std::min<int64_t>(c.ni, std::min<int64_t>(wb, 128));
       c.ni = std::max(c.ni, c.nj);
-      c.K = CH_NB;
+      c.K = Kla;
       c.X = c.Y = A + cp * lda + cb;
       c.ldx = c.ldy = lda;
       c.C = A + cb * lda + cb;
@@ -1632,7 +1745,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       GemmArgs& a = b.la;
       a.ni = std::max<int64_t>((use128 ? std::min<int64_t>(ni, 256) : ni) - 128, 0);
       a.nj = wb;
-      a.K = CH_NB;
+      a.K = Kla;
       a.X = A + cp * lda + cb + 128;
       a.Y = A + cp * lda + cb;
       a.ldx = a.ldy = lda;
@@ -1670,7 +1783,77 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         a.n2c = ds->ns - cb;
       }
       const int64_t m = n - cb - wb;
-      if (m > 0) {
+      b.rag_cp = cb - CH_NB;
+      b.rag_K = CH_NB;
+      if (m > 0 && kind == 1) {
+        // ODD: the rest of the previous EVEN's far region F (origin = this launch's trailing origin),
+        // with that EVEN's pair (columns [cb - 3 CH_NB, cb - CH_NB)); its ragged rows were done there
+        if (bk >= 1 && pl.kind[bk - 1] == 2) {
+          const int64_t me = m + CH_NB;
+          const int64_t rn = (rag_on && me > 128 && (me & 127) != 0 && (me & 127) <= 8) ? (me & 127) : 0;
+          const int64_t mF = m - rn;
+          GemmArgs& g = b.s;
+          g.ni = g.nj = mF;
+          g.K = 2 * CH_NB;
+          g.X = g.Y = A + (cb - 3 * CH_NB) * lda + cb + wb;
+          g.ldx = g.ldy = lda;
+          g.C = A + (cb + wb) * lda + cb + wb;
+          g.ldc = lda;
+          g.sub = 1;
+          g.tri = 1;
+          g.xcd_remap = 1;
+          g.tiles_i = cdiv(mF, 128);
+          g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
+          b.f0 = pl.f1[bk - 1];
+          b.s_full = g.nblk - b.f0;
+          b.ns = b.s_full;
+        }
+      } else if (m > 0 && kind == 2) {
+        // EVEN: strip (block bk+1's columns) + the first f1 tiles of F, both with the pair
+        // (columns [cb - 2 CH_NB, cb)); ragged rows across the whole trailing width
+        int64_t ms = m;
+        if (rag_on && m > 128 && (m & 127) != 0 && (m & 127) <= 8) {
+          ms = m - (m & 127);
+          b.rag_r0 = ms;
+          b.rag_n = (int)(m & 127);
+          b.nrag = (int)cdiv(m, 256);
+          b.rag_cp = cp;
+          b.rag_K = (int)Kla;
+        }
+        const int64_t o = cb + wb, mF = ms - CH_NB;
+        GemmArgs& s2 = b.s2;
+        s2.ni = ms;
+        s2.nj = CH_NB;
+        s2.K = Kla;
+        s2.X = s2.Y = A + cp * lda + o;
+        s2.ldx = s2.ldy = lda;
+        s2.C = A + o * lda + o;
+        s2.ldc = lda;
+        s2.sub = 1;
+        s2.tri = 1;
+        s2.rowmajor = 1;
+        s2.xcd_remap = 0;
+        s2.tiles_i = cdiv(ms, 128);
+        s2.tiles_j = 2;
+        s2.nblk = s2.tiles_i * 2;
+        b.nstrip = s2.nblk - 1;   // (tile (0, 1) lies above the diagonal: skipped)
+        GemmArgs& g = b.s;
+        g = s2;
+        g.rowmajor = 0;
+        g.ni = g.nj = mF;
+        g.X = g.Y = A + cp * lda + o + CH_NB;
+        g.C = A + (o + CH_NB) * lda + o + CH_NB;
+        g.xcd_remap = 1;
+        g.tiles_i = cdiv(mF, 128);
+        g.tiles_j = 0;
+        g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
+        const bool last = bk + 1 >= nblocks || pl.kind[bk + 1] != 1;
+        const int64_t f1 = last ? g.nblk : std::max<int64_t>(0, std::min<int64_t>(g.nblk, (g.nblk - b.nstrip) / 2));
+        pl.f1[bk] = f1;
+        b.f0 = 0;
+        b.s_full = f1;
+        b.ns = b.nstrip + f1;
+      } else if (m > 0) {
         GemmArgs& g = b.s;
         int64_t ms = m;   // tile rows of the trailing update (ragged rows split off below)
         if (rag_on && m > 128 && (m & 127) != 0 && (m & 127) <= 8) {
@@ -1710,27 +1893,28 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
     }
-    if (b.ns > 0 && !defer && split_on) {
+    if (b.s_full > 0 && !defer && split_on) {
       // the planner's split count (cached per size and block: it depends on nothing else)
       static std::mutex mu;
       static std::map<std::pair<int64_t, int64_t>, std::vector<int64_t>> cache;
       const int nchd_h = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
+      const double tc = b.s.K > CH_NB ? 1.6 : 1.0;
       int64_t q = 0;
       {
         std::lock_guard<std::mutex> lk(mu);
         auto& v = cache[{n, ncols}];
         if ((int64_t)v.size() < nblocks) v.assign(nblocks, -1);
         if (v[bk] < 0) {
-          v[bk] = plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.ns, (b.nra - nchd_h) + b.nrb,
-                             potrf_split_cap(n));
+          v[bk] = plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, (b.nra - nchd_h) + b.nrb,
+                             potrf_split_cap(n), tc, b.nstrip, Kla > CH_NB ? 1.6 : 0.8);
           static const bool dbg = getenv("IPM_SPLIT_DEBUG") != nullptr;
           if (dbg) fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld\n", (long)n, (long)bk,
                            (long)b.ns, (long)v[bk]);
         }
         q = v[bk];
       }
-      b.s_full = b.ns - q;
-      b.ns = b.s_full + 2 * q;
+      b.s_full -= q;
+      b.ns = b.nstrip + b.s_full + 2 * q;
       b.sscr = ws + potrf_split_scratch_off(n);
       b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
     }
@@ -1758,6 +1942,10 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       }
       b.gs_total = b.gs_cum[b.ngs];
     }
+    // (IPM_FLEX=1: measured slower, 6.52 -> 7.14 ms at n = 8192 -- row chunks started beside the
+    // MFMA tiles run far slower than at the launch's end; kept as a knob)
+    static const bool flex_on = [] { const char* e = getenv("IPM_FLEX"); return e && e[0] == '1'; }();
+    b.flex = flex_on ? 1 : 0;
     const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)

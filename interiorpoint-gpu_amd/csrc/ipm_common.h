@@ -87,7 +87,7 @@ __host__ __device__ inline int64_t potrf_split_cap(int64_t n) {
   return tri < 512 ? tri : 512;
 }
 __host__ __device__ inline int64_t block_ctl_words(int64_t n) {
-  return 56 + 2 * ((n + 63) / 64) + 8 + potrf_split_cap(n);
+  return 64 + 2 * ((n + 63) / 64) + 8 + potrf_split_cap(n);   // (header: CTL_HDR <= 64 words)
 }
 inline int64_t potrf_split_scratch_off(int64_t n) {
   return ((2 * (8 * 256 + 36 * 256) + (8 + ((n + 127) / 128) * block_ctl_words(n) + 1) / 2 + 8) + 31) & ~int64_t(31);

@@ -78,7 +78,9 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
 #pragma unroll
     for (int q = 0; q < 2; ++q) acc[p][q] = dbl4{0.0, 0.0, 0.0, 0.0};
   // wave wv takes the 4-row slabs kb = 4 wv + 16 j; lane row k = kb + fk.  Four slabs per pass:
-  // 16 independent loads in flight before the 16 MFMAs that consume them.
+  // 16 independent loads in flight before the 16 MFMAs that consume them.  (Issuing the next pass's
+  // loads before this pass's MFMAs -- register double buffering -- measured slower: 47.6 -> 53.4 us
+  // at n = 4097, S = 30, profiles/r3_lasso_pipelined_kernel_stats.csv.)
   constexpr int U = 4;
   for (int64_t kb = kbeg + 4 * wv; kb < kend; kb += 16 * U) {
     double av[U][2], bv[U][2];

@@ -32,6 +32,18 @@
 
 namespace ipm {
 
+// tools/tile_lab.hip only: per-workgroup phase stamps of mfma_tile (wave 0): [0] entry, [1] slab
+// loop start, [2] slab loop end, [3] epilogue stores issued, [4] stores complete (s_memtime
+// cycles); [6] / [7] entry / exit on the 100 MHz clock
+#ifdef IPM_TILE_STAMPS
+__device__ unsigned long long ipm_tile_stamps[4096 * 8];
+#define IPM_TSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) ipm_tile_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define IPM_TSTAMPR(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) ipm_tile_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define IPM_TSTAMP(k) do {} while (0)
+#define IPM_TSTAMPR(k) do {} while (0)
+#endif
+
 struct GemmArgs {
   int64_t ni = 0, nj = 0, K = 0;
   const double* X = nullptr;
@@ -120,6 +132,8 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
                                           int64_t ke = -1) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
+  IPM_TSTAMP(0);
+  IPM_TSTAMPR(6);
   auto& sX = sm.sX;
   auto& sY = sm.sY;
   // ---- tile of this workgroup
@@ -356,6 +370,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     fstore(0);
     fload(nslab > 1 ? 1 : 0);
     __syncthreads();
+    IPM_TSTAMP(1);
     for (int64_t s = 0; s < nslab; ++s) {
       const int buf = (int)(s & 1);
       const double* bx = sX[buf];
@@ -380,6 +395,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
       }
       __syncthreads();
     }
+    IPM_TSTAMP(2);
   } else {
     if (nslab > 0) {
       gload(0);
@@ -482,6 +498,12 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     __syncthreads();
     if (tid == 0) __hip_atomic_store(pflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef IPM_TILE_STAMPS
+  IPM_TSTAMP(3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  IPM_TSTAMP(4);
+  IPM_TSTAMPR(7);
+#endif
 }
 
 // the tile mfma_tile would take for index Lw (same enumeration), and whether it is full with whole

@@ -240,7 +240,9 @@ int main() {
   }
   };
   stamped(k_stamped<130>, 130);
-  stamped(k_stamped<130 + 512>, 642);
+  stamped(k_stamped<130 + 16>, 146);
+  stamped(k_stamped<130 + 32>, 162);
+  stamped(k_stamped<130 + 64>, 194);
 
 
 

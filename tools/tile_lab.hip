@@ -1,6 +1,7 @@
 // Trailing-tile lab (diagnostic only): the Cholesky's trailing update tile (C -= X^T Y, 128 x 128,
 // K = 256, lower-triangle grid, C read first) as shipped vs. variants -- lazy C reads spread over
 // the K loop, persistent workgroups.   scripts/chol_lab.sh runs it.
+#define IPM_TILE_STAMPS 1
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -83,7 +84,26 @@ int main(int argc, char** argv) {
            (long)a.K, name, grid, t[t.size() / 2], fl / (t[t.size() / 2] * 1e-3) / 1e12, t[t.size() / 2] * 1e3 / rounds,
            rounds, t[t.size() / 2] * 1e3 / rounds * 256.0 / a.K, d);
   };
+  auto stamps = [&](const char* name) {
+    std::vector<unsigned long long> st(4096 * 8);
+    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(ipm::ipm_tile_stamps), st.size() * 8));
+    const int nb = (int)std::min<int64_t>(a.nblk, 4096);
+    unsigned long long r0 = ~0ull;
+    for (int b = 0; b < nb; ++b) r0 = std::min(r0, st[b * 8 + 6]);
+    printf("  stamps %s (cycles; per round of 512 workgroups by blockIdx):\n", name);
+    for (int q = 0; q * 512 < nb; ++q) {
+      double pro = 0, loop = 0, epi = 0, drain = 0, t0 = 0, t1 = 0; int c = 0;
+      for (int b = q * 512; b < std::min(nb, q * 512 + 512); ++b, ++c) {
+        const unsigned long long* x = &st[b * 8];
+        pro += x[1] - x[0]; loop += x[2] - x[1]; epi += x[3] - x[2]; drain += x[4] - x[3];
+        t0 += (x[6] - r0) / 100.0; t1 += (x[7] - r0) / 100.0;
+      }
+      printf("    blocks %4d-%4d: prologue %6.0f  slab loop %6.0f  epilogue issue %5.0f  store drain %5.0f | start %.1f us end %.1f us (means)\n",
+             q * 512, q * 512 + c - 1, pro / c, loop / c, epi / c, drain / c, t0 / c, t1 / c);
+    }
+  };
   run(k_tiles<false>, "shipped (C read first)", (int)a.nblk, true);
+  stamps("shipped K=256");
   run(k_tiles<true>, "lazy C (one block per slab)", (int)a.nblk, true);
   run(k_tiles<false>, "shipped, persistent 512 workgroups", 512, true);
   for (long long d : {0LL, 2000LL, 4000LL, 6000LL}) {   // ticks of 10 ns
@@ -102,8 +122,10 @@ int main(int argc, char** argv) {
     a.K = K;
     a.sub = 1; a.alpha = 1.0; a.beta = 0.0;
     run(k_tiles<false>, "C -= X^T Y (C read + write)", (int)a.nblk, false);
+    stamps("C -= X^T Y");
     a.sub = 0; a.alpha = -1.0; a.beta = 0.0;
     run(k_tiles<false>, "C = -X^T Y (write only)", (int)a.nblk, false);
+    stamps("write only");
   }
   return 0;
 }
