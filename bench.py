@@ -185,17 +185,37 @@ def cpu_model():
         return {}
 
 
+def _cpu_worker(argv):
+    """Child process of cpu_baseline: phase-1 Newton iterations of the saved instance with the BLAS
+    thread count fixed by the environment before NumPy loads (OpenBLAS sizes its thread buffers at
+    load time; raising the count in-process past the box's OMP_NUM_THREADS crashed it)."""
+    d, seconds, kw = argv[0], float(argv[1]), json.loads(argv[2])
+    from oracle import ipm_oracle as O
+    C = np.load(os.path.join(d, "C.npy"), mmap_mode="r")
+    C = np.ascontiguousarray(C)
+    dv = np.load(os.path.join(d, "d.npy"))
+    lb = np.load(os.path.join(d, "lb.npy"))
+    ub = np.load(os.path.join(d, "ub.npy"))
+    n = C.shape[1]
+    ph = O.PhaseOne(C=C, d=dv, lb=lb, ub=ub, x0=O.default_x0(n, lb, ub), max_outer_iters=1,
+                    max_inner_iters=1, epsilon=kw["epsilon"], inner_epsilon=1e-5,
+                    alpha=kw["alpha"], beta=kw["beta"], mu=kw["mu"], t0=0.01, n=n, tol=0)
+    iters, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0 < seconds or iters == 0) and iters < 200:
+        ph.x, _, k, _, _ = ph.ns.solve(ph.x, 0.01)
+        iters += k
+    el = time.perf_counter() - t0
+    print(json.dumps({"iters": iters, "seconds": el, "blas": blas_info()}), flush=True)
+
+
 def cpu_baseline(inst, kwargs, seconds):
     """Oracle (NumPy/SciPy restatement, oracle/ipm_oracle.py) on a bounded sample of the same
     workload: phase-1 Newton iterations of this instance (bordered n+1 SYRK + Cholesky + solves),
     at 1 BLAS thread, at the box's CPU share (OMP_NUM_THREADS) and at the physical core count, ~`seconds` each
-    (>= 1 iteration); the fastest is the baseline."""
-    from threadpoolctl import threadpool_limits
-
-    from oracle import ipm_oracle as O
+    (>= 1 iteration); the fastest is the baseline.  Each thread count runs in its own child process
+    (_cpu_worker) with the count set in its environment; a failing child is recorded, not fatal."""
+    import tempfile
     n = len(inst["q"])
-    lb = np.array(inst["lower_bound"], dtype=float)
-    ub = np.array(inst["upper_bound"], dtype=float)
     avail = len(os.sched_getaffinity(0))
     cap = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
     # 1 thread, the box's CPU share (OMP_NUM_THREADS), and every physical core of the host
@@ -206,24 +226,41 @@ def cpu_baseline(inst, kwargs, seconds):
     except ValueError:
         phys = 0
     nthreads = sorted({1, max(1, min(avail, cap))} | ({min(avail, phys)} if phys > 0 else set()))
-    runs = []
-    for nt in nthreads:
-        with threadpool_limits(limits=nt, user_api="blas"):
-            ph = O.PhaseOne(C=inst["C"], d=inst["d"], lb=lb, ub=ub, x0=O.default_x0(n, lb, ub), max_outer_iters=1,
-                            max_inner_iters=1, epsilon=kwargs["epsilon"], inner_epsilon=1e-5,
-                            alpha=kwargs["alpha"], beta=kwargs["beta"], mu=kwargs["mu"], t0=0.01, n=n, tol=0)
-            iters, t0 = 0, time.perf_counter()
-            while (time.perf_counter() - t0 < seconds or iters == 0) and iters < 200:
-                ph.x, _, k, _, _ = ph.ns.solve(ph.x, 0.01)
-                iters += k
-            el = time.perf_counter() - t0
-        runs.append({"threads": nt, "iters": iters, "seconds": el, "value": iters / el})
+    runs, fails, blas = [], [], {}
+    kw = json.dumps({k: kwargs[k] for k in ("epsilon", "alpha", "beta", "mu")})
+    with tempfile.TemporaryDirectory(prefix="ipm_cpu_") as td:
+        np.save(os.path.join(td, "C.npy"), np.asarray(inst["C"], dtype=np.float64))
+        np.save(os.path.join(td, "d.npy"), np.asarray(inst["d"], dtype=np.float64))
+        np.save(os.path.join(td, "lb.npy"), np.asarray(inst["lower_bound"], dtype=np.float64))
+        np.save(os.path.join(td, "ub.npy"), np.asarray(inst["upper_bound"], dtype=np.float64))
+        for nt in nthreads:
+            env = dict(os.environ)
+            for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+                env[k] = str(nt)
+            try:
+                r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-worker", td, str(seconds), kw],
+                                   env=env, capture_output=True, text=True, timeout=max(120.0, 10 * seconds))
+                if r.returncode != 0:
+                    fails.append({"threads": nt, "rc": r.returncode, "stderr": r.stderr[-300:]})
+                    continue
+                o = json.loads(r.stdout.strip().splitlines()[-1])
+            except Exception as e:   # noqa: BLE001  (a baseline failure must not sink the bench line)
+                fails.append({"threads": nt, "error": repr(e)[:300]})
+                continue
+            blas = o.get("blas") or blas
+            runs.append({"threads": nt, "iters": o["iters"], "seconds": o["seconds"],
+                         "value": o["iters"] / o["seconds"]})
+    if not runs:
+        return {"value": None, "unit": "Newton iters/s", "cores": 0, "kind": "port", "failed": fails}
     best = max(runs, key=lambda r: r["value"])   # the fastest thread count is the baseline
-    return {"value": best["value"], "unit": "Newton iters/s", "cores": best["threads"], "kind": "port",
-            "sample": f"{best['iters']} phase-1 Newton iterations (bordered n+1={n + 1} KKT, m={len(inst['d'])}) of "
-                      f"the same instance, oracle/ipm_oracle.py on NumPy/OpenBLAS, {best['seconds']:.1f} s",
-            "by_threads": runs, "host": {"os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
-                                         "physical_cores": phys, "lscpu": lc, "blas": blas_info()}}
+    out = {"value": best["value"], "unit": "Newton iters/s", "cores": best["threads"], "kind": "port",
+           "sample": f"{best['iters']} phase-1 Newton iterations (bordered n+1={n + 1} KKT, m={len(inst['d'])}) of "
+                     f"the same instance, oracle/ipm_oracle.py on NumPy/OpenBLAS, {best['seconds']:.1f} s",
+           "by_threads": runs, "host": {"os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+                                        "physical_cores": phys, "lscpu": lc, "blas": blas}}
+    if fails:
+        out["failed"] = fails
+    return out
 
 
 def main():
@@ -459,4 +496,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
+        _cpu_worker(sys.argv[2:])
+    else:
+        main()

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <queue>
 #include <cmath>
+#include <tuple>
 #include <vector>
 #include <cstdlib>
 
@@ -662,8 +663,66 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     //      rank-1 updates (one v_fmac_f64 with a DPP row broadcast of column c each) run beside it.
     //      Wave 1 joins (a redundant copy of the chain) for the tiles wave 0 has no group for.
     const int nbt = 7 - J;                                   // tiles below the diagonal one
-    const bool leafw = (wv == 0) || (wv == 1 && nbt > 4);
-    if (leafw) {
+    // V & 32768 (one register stream): group 0 of each leaf wave holds the diagonal block's rows,
+    // groups 1-3 the rows of three tiles below; the multipliers L[c2][c] come from group 0 through
+    // SGPRs (v_readlane), so diagonal and tile rows share ONE v_fma per column pair instead of a
+    // DPP fmac on a copy of the diagonal rows plus a second one on the tile rows.  Bitwise the
+    // same arithmetic as the two-stream sweep (same fma operands).  Leaf waves: 0, 1 while more
+    // than 3 tiles are below, 2 for the seventh (J = 0, when waves 2-3 have no other work).
+    constexpr bool ONE = (V & 32768) != 0;
+    const bool leafw = ONE ? (wv == 0 || (wv == 1 && nbt > 3) || (wv == 2 && nbt > 6))
+                           : ((wv == 0) || (wv == 1 && nbt > 4));
+    if (ONE && leafw) {
+      const int db = bidx(J, J) * 256;
+      const int rr = lane & 15, g = lane >> 4;
+      const int It = J + 3 * wv + g;                         // g >= 1: this lane group's tile
+      const bool tval = g > 0 && It < 8;
+      const int src = tval ? bidx(It, J) * 256 : db;         // absent tiles: a harmless diagonal copy
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = sD[src + c * 16 + rr];
+      int bad = 0;
+      double dvs[16];
+      double piv = readlane_d(row[0], 0);
+      double dv = rsqrt_pivot(piv);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        dvs[c] = dv;
+        double pivn = 1.0, dvn = 1.0;
+        if (c + 1 < 16) {
+          const double a1 = readlane_d(row[c], c + 1);
+          const double d1 = readlane_d(row[c + 1], c + 1);
+          const double l1 = a1 * dv;
+          pivn = fma(-l1, l1, d1);
+          dvn = rsqrt_pivot(pivn);
+        }
+        row[c] *= dv;   // diagonal lane c: L_cc; other diagonal lanes: L[r][c]; tile lanes: X[r][c]
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) row[c2] = fma(-readlane_d(row[c], c2), row[c], row[c2]);
+        piv = pivn;
+        dv = dvn;
+      }
+      if (tval) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          sD[src + c * 16 + rr] = row[c];
+          if (pubL) st_sc1(&pubL[src + c * 16 + rr], row[c]);
+        }
+      }
+      if (wv == 0) {
+        double mine = dvs[0];
+#pragma unroll
+        for (int c = 1; c < 16; ++c) mine = (lane == c) ? dvs[c] : mine;
+        if (lane < 16) {
+          srinv[J * 16 + lane] = mine;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = (rr >= c) ? row[c] : 0.0;   // column-major
+        }
+        if (lane == 0 && bad) fail = J * 16 + bad;
+      }
+      STAMPAT(32 + J);
+    } else if (leafw) {
       const int db = bidx(J, J) * 256;
       const int rr = lane & 15;
       const int Ib = J + 1 + 4 * wv + (lane >> 4);
@@ -794,7 +853,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       STAMPAT(64 + 8 * wv + J);
       // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin.  V & 128: wave 3 (the
       // inverse, ~3900 cycles) takes no look-ahead tiles -- they go to the other free waves
-      const int f0 = nbt > 4 ? 2 : 1;
+      const int f0 = (ONE ? nbt > 3 : nbt > 4) ? 2 : 1;
       const int nf = (V & 128) ? 3 - f0 : 4 - f0;
       if (V & 256) {
         // greedy list schedule of the look-ahead tiles I = J+1..7 over the free waves, by cost
@@ -1118,6 +1177,13 @@ struct BlockArgs {
   int rag_K = CH_NB;            // ragged rows: K extent and first column of the applied blocks
   int64_t rag_cp = 0;
   int flex = 0;                 // IPM_FLEX: trailing tiles and non-critical row chunks share tickets
+  // trailing tiles around the non-critical row chunks (row_slots): S tickets [0, sa), the other
+  // P(a) row chunks, S [sa, sb), the P(b) row chunks, S [sb, ns).  sa = sb = ns: rows last.
+  // rpad_a / rpad_b: no-op tickets after each row group placed among the S tiles, so that the
+  // S tickets keep their ticket-mod-8 XCD phase (the XCD-contiguous tile runs, xcd_remap)
+  int64_t sa = 0, sb = 0;
+  int rpad_a = 0, rpad_b = 0;
+  int rowprio = 0;              // s_setprio of the non-critical row chunks (IPM_ROWPRIO)
 };
 #ifndef FLEX_PROG
 #define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
@@ -1342,16 +1408,26 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         }
       } else if (b.flex) {
         if ((t -= b.ns + na + b.nrb) < b.gs_total) kind = K_GS;
-      } else if ((t -= b.nrag) < b.ns) {
+      } else if ((t -= b.nrag) < b.sa) {
         kind = K_TILE;
-      } else if ((t -= b.ns) < na) {
-        kind = K_ROW;
-        chunk = nchd + t;
-      } else if ((t -= na) < b.nrb) {
-        kind = K_ROW;
-        pb = true;
-        chunk = t;
-      } else if ((t -= b.nrb) < b.gs_total) {
+      } else if ((t -= b.sa) < na + b.rpad_a) {
+        if (t < na) {   // (else a padding ticket: nothing)
+          kind = K_ROW;
+          chunk = nchd + t;
+        }
+      } else if ((t -= na + b.rpad_a) < b.sb - b.sa) {
+        kind = K_TILE;
+        t += b.sa;
+      } else if ((t -= b.sb - b.sa) < b.nrb + b.rpad_b) {
+        if (t < b.nrb) {
+          kind = K_ROW;
+          pb = true;
+          chunk = t;
+        }
+      } else if ((t -= b.nrb + b.rpad_b) < b.ns - b.sb) {
+        kind = K_TILE;
+        t += b.sb;
+      } else if ((t -= b.ns - b.sb) < b.gs_total) {
         kind = K_GS;   // last: they fill the CUs the chain leaves idle
       }
     }
@@ -1383,6 +1459,10 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   }
   if (kind == K_ROW) {
     ROLE(pb ? 6 : (chunk < nchd ? 2 : 5));
+    // (latency-bound MFMA chains: beside trailing tiles they win the issue arbitration)
+    if (b.rowprio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (b.rowprio == 2) __builtin_amdgcn_s_setprio(2);
+    else if (b.rowprio >= 3) __builtin_amdgcn_s_setprio(3);
     if (pb) {
       // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
       const int64_t r0 = b.wbw + chunk * PF_RB;
@@ -1627,15 +1707,89 @@ static double split_makespan(int slots, const std::vector<std::pair<int64_t, dou
 }
 // (pair launches, K = 512: tiles cost tc = 1.6 (tools/tile_lab.hip: 154 vs 96 us), look-ahead
 // tiles twice their K = 256 cost, and the nstrip strip tiles come first)
+// S tickets [0, ns_all) = nstrip strips, ns - q whole tiles, 2 q halves; the non-critical row
+// chunks (nra of P(a), nrb of P(b)) go before S tickets sa and sb
+static std::vector<std::pair<int64_t, double>> launch_items(int64_t nla, int64_t nchd, int64_t nnf, bool pb,
+                                                            int64_t nrag, int64_t nstrip, int64_t ns, int64_t q,
+                                                            double tc, double lac, int64_t nra, int64_t nrb,
+                                                            int64_t sa, int64_t sb) {
+  std::vector<std::pair<int64_t, double>> it = {{nla, lac}, {1, 0.6}, {nchd, 0.66}, {nnf, 0.8}, {pb ? 1 : 0, 1.25},
+                                                {nrag, 0.1 * tc}};
+  // S pieces: [begin, end) in S-ticket index with a duration
+  const int64_t e1 = nstrip + ns - q, e2 = e1 + 2 * q;
+  auto span = [&](int64_t a, int64_t z) {
+    const int64_t w1 = std::max<int64_t>(0, std::min(z, e1) - a);
+    const int64_t w2 = std::max<int64_t>(0, std::min(z, e2) - std::max(a, e1));
+    if (w1 > 0) it.push_back({w1, tc});
+    if (w2 > 0) it.push_back({w2, 0.55 * tc});
+  };
+  sa = std::min(sa, e2);
+  sb = std::min(std::max(sb, sa), e2);
+  span(0, sa);
+  it.push_back({nra, 0.5});
+  span(sa, sb);
+  it.push_back({nrb, 0.5});
+  span(sb, e2);
+  return it;
+}
+// ---- where the non-critical row chunks go among the trailing tiles (IPM_ROWPOS=1).  The rest of
+// P(a)'s row chunks can run once its diagonal role is done (~0.7 tile units into a launch), P(b)'s
+// once its own is (~1.3, role timelines in DESIGN.md).  Queued behind every trailing tile they all
+// start in the last round and hold the launch open after the tiles drain (block 4 of n = 8192:
+// the last 85 of 415 us); here each goes before the first S ticket the list schedule dispatches
+// after its panel is ready.  sa = sb = ns_all keeps them last.
+static void row_slots(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t nstrip, int64_t ns_all,
+                      double tc, double lac, int64_t nra, double ta, double tb, int64_t& sa, int64_t& sb) {
+  sa = sb = ns_all;
+  if (ns_all < 64) return;
+  const int slots = 2 * num_cus();
+  std::priority_queue<double, std::vector<double>, std::greater<double>> h;
+  for (int i = 0; i < slots; ++i) h.push(0.0);
+  auto run = [&](int64_t cnt, double d) {
+    for (int64_t k = 0; k < cnt; ++k) {
+      const double t0 = h.top();
+      h.pop();
+      h.push(t0 + d);
+    }
+  };
+  run(nla, lac);
+  run(1, 0.6);
+  run(nchd, 0.66);
+  run(nnf, 0.8);
+  run(pb ? 1 : 0, 1.25);
+  run(nrag, 0.1 * tc);
+  bool placed_a = false;
+  int64_t i = 0;
+  while (i < ns_all) {
+    const double t0 = h.top();
+    if (!placed_a && t0 >= ta) {
+      sa = i;
+      placed_a = true;
+      run(nra, 0.5);
+      continue;   // (the rows took slots: re-read the next dispatch time)
+    }
+    if (placed_a && t0 >= tb) {
+      sb = i;
+      return;
+    }
+    h.pop();
+    h.push(t0 + tc);
+    ++i;
+  }
+}
 static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t ns, int64_t nrows,
-                          int64_t cap, double tc = 1.0, int64_t nstrip = 0, double lac = 0.8) {
+                          int64_t cap, double tc = 1.0, int64_t nstrip = 0, double lac = 0.8, int64_t nra = -1,
+                          int64_t sa = -1, int64_t sb = -1) {
   if (ns < 64) return 0;
   const int slots = 2 * num_cus();
+  if (nra < 0) {   // rows last
+    nra = nrows;
+    sa = sb = nstrip + ns;
+  }
+  const int64_t nrb = nrows - nra;
   auto mk = [&](int64_t q) {
-    std::vector<std::pair<int64_t, double>> it = {{nla, lac}, {1, 0.6}, {nchd, 0.66}, {nnf, 0.8}, {pb ? 1 : 0, 1.25},
-                                                  {nrag, 0.1 * tc}, {nstrip, tc}, {ns - q, tc}, {2 * q, 0.55 * tc},
-                                                  {nrows, 0.5}};
-    return split_makespan(slots, it);
+    int64_t a = sa, z = sb;
+    return split_makespan(slots, launch_items(nla, nchd, nnf, pb, nrag, nstrip, ns, q, tc, lac, nra, nrb, a, z));
   };
   const double m0 = mk(0);
   double best = m0;
@@ -1893,31 +2047,56 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
     }
-    if (b.s_full > 0 && !defer && split_on) {
-      // the planner's split count (cached per size and block: it depends on nothing else)
+    static const bool flex_on = [] { const char* e = getenv("IPM_FLEX"); return e && e[0] == '1'; }();
+    // IPM_ROWPOS=1: the non-critical row chunks among the trailing tiles (row_slots)
+    static const bool rowpos_on = [] { const char* e = getenv("IPM_ROWPOS"); return e && e[0] == '1'; }();
+    b.sa = b.sb = b.ns;
+    if (b.s_full > 0 && !defer && (split_on || rowpos_on)) {
+      // the planner's split count and row positions (cached per size and block: they depend on
+      // nothing else)
+      struct Plan { int64_t q = -1, sa = 0, sb = 0; };
       static std::mutex mu;
-      static std::map<std::pair<int64_t, int64_t>, std::vector<int64_t>> cache;
+      static std::map<std::tuple<int64_t, int64_t, int>, std::vector<Plan>> cache;
       const int nchd_h = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-      const double tc = b.s.K > CH_NB ? 1.6 : 1.0;
-      int64_t q = 0;
+      const double tc = b.s.K > CH_NB ? 1.6 : 1.0, lac = Kla > CH_NB ? 1.6 : 0.8;
+      const int64_t nra_h = b.nra - nchd_h;
+      Plan p;
       {
         std::lock_guard<std::mutex> lk(mu);
-        auto& v = cache[{n, ncols}];
-        if ((int64_t)v.size() < nblocks) v.assign(nblocks, -1);
-        if (v[bk] < 0) {
-          v[bk] = plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, (b.nra - nchd_h) + b.nrb,
-                             potrf_split_cap(n), tc, b.nstrip, Kla > CH_NB ? 1.6 : 0.8);
+        auto& v = cache[{n, ncols, (split_on ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0)}];
+        if ((int64_t)v.size() < nblocks) v.assign(nblocks, Plan{});
+        if (v[bk].q < 0) {
+          Plan& w = v[bk];
+          w.sa = w.sb = b.ns;
+          if (rowpos_on && !flex_on) {
+            static const double ta = [] { const char* e = getenv("IPM_ROW_TA"); return e ? atof(e) : 0.75; }();
+            static const double tb = [] { const char* e = getenv("IPM_ROW_TB"); return e ? atof(e) : 1.35; }();
+            row_slots(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.nstrip, b.ns, tc, lac, nra_h, ta, tb, w.sa, w.sb);
+          }
+          w.q = split_on ? plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, nra_h + b.nrb,
+                                      potrf_split_cap(n), tc, b.nstrip, lac, nra_h, w.sa, w.sb)
+                         : 0;
           static const bool dbg = getenv("IPM_SPLIT_DEBUG") != nullptr;
-          if (dbg) fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld\n", (long)n, (long)bk,
-                           (long)b.ns, (long)v[bk]);
+          if (dbg)
+            fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld, rows before S %ld / %ld\n",
+                    (long)n, (long)bk, (long)b.ns, (long)w.q, (long)w.sa, (long)w.sb);
         }
-        q = v[bk];
+        p = v[bk];
       }
-      b.s_full -= q;
-      b.ns = b.nstrip + b.s_full + 2 * q;
-      b.sscr = ws + potrf_split_scratch_off(n);
-      b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
+      b.s_full -= p.q;
+      b.ns = b.nstrip + b.s_full + 2 * p.q;
+      b.sa = std::min(p.sa, b.ns);
+      b.sb = std::min(std::max(p.sb, b.sa), b.ns);
+      static const bool rpad_on = [] { const char* e = getenv("IPM_ROWPAD"); return !(e && e[0] == '0'); }();
+      if (rpad_on && b.sa < b.ns) b.rpad_a = (8 - (b.nra - nchd_h) % 8) % 8;
+      if (rpad_on && b.sb < b.ns) b.rpad_b = (8 - b.nrb % 8) % 8;
+      if (split_on) {
+        b.sscr = ws + potrf_split_scratch_off(n);
+        b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
+      }
     }
+    static const int rowprio = [] { const char* e = getenv("IPM_ROWPRIO"); return e ? atoi(e) : 0; }();
+    b.rowprio = rowprio;
     if (defer) {
       // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
       b.gX = ds->X;
@@ -1944,9 +2123,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     }
     // (IPM_FLEX=1: measured slower, 6.52 -> 7.14 ms at n = 8192 -- row chunks started beside the
     // MFMA tiles run far slower than at the launch's end; kept as a knob)
-    static const bool flex_on = [] { const char* e = getenv("IPM_FLEX"); return e && e[0] == '1'; }();
     b.flex = flex_on ? 1 : 0;
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total;
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total +
+                         b.rpad_a + b.rpad_b;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
     static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();

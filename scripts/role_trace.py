@@ -29,7 +29,7 @@ print(f"block {os.environ.get('IPM_TRACE_BLOCK')} n={n}: {len(a)} workgroups, sp
 for r in sorted(set((a[:, 0] >> 32).tolist())):
     s = a[(a[:, 0] >> 32) == r]
     d = (s[:, 2] - s[:, 1]) / 100
-    print(f"  {names.get(r, r):14s} n={len(s):5d} start {(s[:, 1].min() - t0) / 100:7.1f}..{(s[:, 1].max() - t0) / 100:7.1f}"
+    print(f"  {str(names.get(r, r)):14s} n={len(s):5d} start {(s[:, 1].min() - t0) / 100:7.1f}..{(s[:, 1].max() - t0) / 100:7.1f}"
           f"  end {(s[:, 2].min() - t0) / 100:7.1f}..{(s[:, 2].max() - t0) / 100:7.1f}  dur mean {d.mean():6.1f} max {d.max():6.1f}")
 print(f"  distinct CU keys {len(set(a[:, 3].tolist()))}")
 # S-tile durations by start time (are mid-launch tiles, with no panel work beside them, slower?)
