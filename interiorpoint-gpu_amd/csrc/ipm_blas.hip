@@ -1807,7 +1807,7 @@ static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64
 // e+1 (look-ahead: block e, K = 256; trailing: the rest of F with the pair e-2, e-1).  The launch
 // before the first EVEN is an ODD with nothing to apply (its chain runs without trailing work once);
 // the last EVEN takes all of F and plain launches follow.  Pairs run while F has at least
-// IPM_PAIR_MIN rows (default 3072: trailing-bound launches); IPM_PAIR=0 turns them off.
+// IPM_PAIR_MIN rows (default 6144: the first, most trailing-bound launches); IPM_PAIR=0 turns them off.
 struct PairPlan {
   std::vector<int> kind;      // per 256-column block
   std::vector<int64_t> f1;    // EVEN: F tiles it takes (tile list [0, f1)); ODD: the EVEN's f1
@@ -1816,10 +1816,12 @@ static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks, bool 
   PairPlan pl;
   pl.kind.assign(nblocks, 0);
   pl.f1.assign(nblocks, 0);
-  // (off by default: measured 6.49 -> 6.73 ms at n = 8192, r3 pair_ab -- the early pairs gain ~0.4 ms,
-  // the later ones lose more: their K = 512 tiles fill one round and the row chunks queue behind)
-  static const bool on = [] { const char* e = getenv("IPM_PAIR"); return e && e[0] == '1'; }();
-  static const int64_t minrows = [] { const char* e = getenv("IPM_PAIR_MIN"); return e ? atoll(e) : 3072LL; }();
+  // Pairs pay only while the far region is large: at n = 8192 with F >= 3072 rows (five pairs) they
+  // were slower, 6.49 -> 6.73 ms (the later pairs' K = 512 tiles fill one round and the row chunks
+  // queue behind); F >= 6144 (three pairs, launches 1-6) is the best threshold of the r3 sweep,
+  // 6.40 -> 6.22 ms (6656: 6.31, 5632: 6.35; profiles/r3_pair_sweep.txt).  IPM_PAIR=0: off.
+  static const bool on = [] { const char* e = getenv("IPM_PAIR"); return !(e && e[0] == '0'); }();
+  static const int64_t minrows = [] { const char* e = getenv("IPM_PAIR_MIN"); return e ? atoll(e) : 6144LL; }();
   if (!on || defer || ncols < n - 8) return pl;   // (a partial factorisation keeps the plain order)
   // EVEN e needs block e+1 to exist and F = rows beyond block e+1 of at least minrows
   int64_t last = -1;
