@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/ipm355.h"
@@ -399,9 +400,11 @@ extern "C" int ipm_lasso_loss(ipm_handle* h, const ipm_lasso_args* a, int absm, 
 // K split of the iteration GEMM: enough workgroups for the chip (>= ~512), chunks of >= 128 rows
 static int admm_ksplit(int64_t n, int64_t S) {
   const int64_t tiles = ((S + LT - 1) / LT) * ((n + LT - 1) / LT);
-  int64_t ks = (512 + tiles - 1) / tiles;
+  // IPM_ADMM_WG: the workgroup target (default 512)
+  static const int64_t target = [] { const char* e = getenv("IPM_ADMM_WG"); return e ? atoll(e) : 512LL; }();
+  int64_t ks = (target + tiles - 1) / tiles;
   ks = std::min<int64_t>(ks, std::max<int64_t>(n / 128, 1));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(ks, 8));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(ks, 16));
 }
 
 // [norm partials: 4 per tile + 8][K-split partial tiles][K-split counters (as doubles)]; must be

@@ -70,6 +70,59 @@ __global__ __launch_bounds__(64) void k_sweep(const double* io, double* out, uns
   out[lane] = acc;
 }
 
+// one register stream (diag_role V & 32768): group 0 diagonal rows, groups 1-3 tile rows, the
+// multipliers through SGPRs (v_readlane); R: 0 = readlane per (c, c2), 1 = the column's multipliers
+// read first, then the fmas
+template <int R>
+__global__ __launch_bounds__(64) void k_sweep_one(const double* io, double* out, unsigned long long* cyc, int reps) {
+  const int lane = threadIdx.x & 63, rr = lane & 15, g = lane >> 4;
+  const double zero = io[512];
+  double orig[16], row[16];
+  for (int c = 0; c < 16; ++c) {
+    orig[c] = io[(g ? 256 : 0) + c * 16 + rr];
+    row[c] = orig[c];
+  }
+  double acc = 0.0;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < reps; ++it) {
+    double piv = ipm::readlane_d(row[0], 0);
+    double dv = ipm::rsqrt_pivot(piv);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      acc += dv;
+      double pivn = 1.0, dvn = 1.0;
+      if (c + 1 < 16) {
+        const double a1 = ipm::readlane_d(row[c], c + 1);
+        const double d1 = ipm::readlane_d(row[c + 1], c + 1);
+        const double l1 = a1 * dv;
+        pivn = fma(-l1, l1, d1);
+        dvn = ipm::rsqrt_pivot(pivn);
+      }
+      row[c] *= dv;
+      if (R == 0) {
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) row[c2] = fma(-ipm::readlane_d(row[c], c2), row[c], row[c2]);
+      } else {
+        double m[16];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) m[c2] = ipm::readlane_d(row[c], c2);
+#pragma unroll
+        for (int c2 = c + 1; c2 < 16; ++c2) row[c2] = fma(-m[c2], row[c], row[c2]);
+      }
+      piv = pivn;
+      dv = dvn;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      acc += row[c];
+      row[c] = fma(row[c], zero, orig[c]);
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) cyc[0] = (t1 - t0) / reps;
+  out[lane] = acc;
+}
+
 // the tile-below row update of the leaf in several forms (diag rows keep the shipped DPP fmac);
 // F 0 shipped (v_fmac_f64_dpp rowb, -row_bcast, rowb), 1 readlane -> SGPR multiplier + v_fma,
 // 2 asm v_mov_b64_dpp + v_fma, 3 builtin update_dpp + v_fma, 4 shipped with an s_nop 1 before every
@@ -240,9 +293,7 @@ int main() {
   }
   };
   stamped(k_stamped<130>, 130);
-  stamped(k_stamped<130 + 16>, 146);
-  stamped(k_stamped<130 + 32>, 162);
-  stamped(k_stamped<130 + 64>, 194);
+  stamped(k_stamped<130 + 32768>, 130 + 32768);
 
 
 
@@ -260,7 +311,9 @@ int main() {
     hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
     printf("%-46s %6llu cycles per 16-column sweep (incl. restore)\n", name, c);
   };
-  if (0) sweep(k_sweep<0>, "sweep as shipped (diag + tile-below rows)");
+  sweep(k_sweep<0>, "sweep as shipped (diag + tile-below rows)");
+  sweep(k_sweep_one<0>, "one stream, readlane per fma");
+  sweep(k_sweep_one<1>, "one stream, column multipliers first");
   sweep(k_sweep<1>, "diag rows only");
   sweep(k_sweep<2>, "pivot chain only");
   if (0) sweep(k_sweep<3>, "rank-1 DPP updates only (both row sets)");
