@@ -1267,7 +1267,10 @@ struct RoleTrace {
 
 // FASTS: every trailing tile of this launch is a full 128-tile (K = 256): they run the
 // branch-free slab loop (mfma_tile LOOP 1) -- one instantiation per kernel, as the allocator needs
-template <bool VEC, bool FASTS = false>
+// LAZY (default; IPM_LAZYC=0 turns it off.  FASTS launches whose trailing tiles are all whole K = 256 tiles, no strips or
+// K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
+// before the first MFMA
+template <bool VEC, bool FASTS = false, bool LAZY = false>
 __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ BlockSmem sm;
   __shared__ int sticket, sflag;
@@ -1659,7 +1662,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         }
         // (both loops in one kernel raised the SGPR spills 89 -> 621 and cost 2.5 %: the launch
         // picks the kernel instead, FASTS)
-        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0>(
+        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0, LAZY && FASTS && VEC>(
             g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
                      : b.f0 + (u < 0 ? st : b.s_full + p),
             sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
@@ -2132,7 +2135,11 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     // branch-free tile loop (IPM_FASTS=0: never)
     static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
-    if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    // (r3 A/B, two pairs: 6.48 / 6.52 -> 6.41 / 6.44 ms at the bordered n = 8193; IPM_LAZYC=0: off)
+    static const bool lazy_on = [] { const char* e = getenv("IPM_LAZYC"); return !(e && e[0] == '0'); }();
+    const bool lazy = lazy_on && fasts && b.s.K == CH_NB && b.nstrip == 0 && b.s_full == b.ns;
+    if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    else if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec) hipLaunchKernelGGL((k_potrf_block<true, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else hipLaunchKernelGGL((k_potrf_block<false, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
   }
