@@ -54,7 +54,7 @@ struct AdmmStep {
   int ba_bcast = 0, eta_bcast = 0, positive = 0, add_bias = 0, dual_form = 0;
 };
 
-template <bool CHECK>
+template <bool CHECK, int U = 4>
 __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __restrict__ W, double* __restrict__ Wn) {
   __shared__ double red[4][LT * (LT + 1)];
   __shared__ double bred[16];
@@ -82,7 +82,6 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
   // 16 independent loads in flight before the 16 MFMAs that consume them.  (Issuing the next pass's
   // loads before this pass's MFMAs -- register double buffering -- measured slower: 47.6 -> 53.4 us
   // at n = 4097, S = 30, profiles/r3_lasso_pipelined_kernel_stats.csv.)
-  constexpr int U = 4;
   for (int64_t kb = kbeg + 4 * wv; kb < kend; kb += 16 * U) {
     double av[U][2], bv[U][2];
 #pragma unroll
@@ -455,8 +454,18 @@ extern "C" int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* i
   int it = 0;
   for (; it < a->max_iters; ++it) {
     const bool check = it % a->check_stop == a->check_stop - 1;
-    if (check) hipLaunchKernelGGL(k_admm_step<true>, grid, dim3(256), 0, st, s, W, Wn);
-    else hipLaunchKernelGGL(k_admm_step<false>, grid, dim3(256), 0, st, s, W, Wn);
+    // IPM_ADMM_U: 4-row slabs per wave and pass (loads in flight before the MFMAs that use them)
+    static const int U = [] { const char* e = getenv("IPM_ADMM_U"); return e ? atoi(e) : 4; }();
+    if (U == 8) {
+      if (check) hipLaunchKernelGGL((k_admm_step<true, 8>), grid, dim3(256), 0, st, s, W, Wn);
+      else hipLaunchKernelGGL((k_admm_step<false, 8>), grid, dim3(256), 0, st, s, W, Wn);
+    } else if (U == 16) {
+      if (check) hipLaunchKernelGGL((k_admm_step<true, 16>), grid, dim3(256), 0, st, s, W, Wn);
+      else hipLaunchKernelGGL((k_admm_step<false, 16>), grid, dim3(256), 0, st, s, W, Wn);
+    } else {
+      if (check) hipLaunchKernelGGL((k_admm_step<true, 4>), grid, dim3(256), 0, st, s, W, Wn);
+      else hipLaunchKernelGGL((k_admm_step<false, 4>), grid, dim3(256), 0, st, s, W, Wn);
+    }
     std::swap(W, Wn);
     if (a->compute_loss) {
       const int rc = ipm_lasso_loss(h, a, a->positive ? 0 : 1, a->gaps + (int64_t)it * a->ldg, a->gap_cols);
