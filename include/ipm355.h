@@ -273,6 +273,7 @@ typedef struct ipm_lasso_args {
   double* gaps;            /* [dev] max_iters rows of ldg: gaps[it*ldg + col(s)]               */
   int64_t ldg;
   const int64_t* gap_cols; /* [dev] S: column of problem s in gaps (chunks), NULL: s            */
+  int32_t qs_blocked;      /* 1: Qs is the tile-blocked copy of ipm_lasso_block_qs (ldq unused)  */
 } ipm_lasso_args;
 
 /* row-major C (M x N, ldc) = alpha A^T B + beta C; A: K x M (lda), B: K x N (ldb); fp64 MFMA */
@@ -298,6 +299,12 @@ int ipm_lasso_prox(ipm_handle* h, int64_t n, int64_t S, const double* v, int64_t
 /* loss per problem of the current alpha into out[cols ? cols[s] : s]; absm: |alpha| in the l1 term */
 int ipm_lasso_loss(ipm_handle* h, const ipm_lasso_args* a, int absm, double* out, const int64_t* cols);
 int64_t ipm_lasso_partial_doubles(int64_t n, int64_t S);
+/* Qs (n x n, ldq, k-major) -> Qb in the ADMM step's tile-blocked layout: 32-row tiles of i, each
+   tile's k rows contiguous (element (i, k) at ((i / 32) * n + k) * 32 + i % 32, rows >= n zero), so
+   that each workgroup of the iteration GEMM streams one contiguous span instead of 256-byte pieces
+   of every k row.  Qb holds ipm_lasso_qb_doubles(n) doubles. */
+int64_t ipm_lasso_qb_doubles(int64_t n);
+int ipm_lasso_block_qs(ipm_handle* h, int64_t n, const double* Qs, int64_t ldq, double* Qb);
 /* the ADMM loop (LassoSolver.py:240-337, one chunk of :339-485): iterates until the stopping
    test (every check_stop iterations) or max_iters; *iters = the last iteration index */
 int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* iters);

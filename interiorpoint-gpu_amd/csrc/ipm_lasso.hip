@@ -52,6 +52,7 @@ struct AdmmStep {
   unsigned* kcnt = nullptr;     // K-split arrivals per tile (the last one finishes the tile, resets it)
   double rho = 0.0;
   int ba_bcast = 0, eta_bcast = 0, positive = 0, add_bias = 0, dual_form = 0;
+  int qs_blocked = 0;           // Qs tile-blocked (ipm_lasso_block_qs): tile y's k rows contiguous
 };
 
 template <bool CHECK, int U = 4>
@@ -67,7 +68,10 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
     iin[t] = i0 + 16 * t + fr < n;
     sin_[t] = s0 + 16 * t + fr < S;
   }
-  const double* qp = a.Qs + i0 + fr;
+  // k row stride of Qs: the tile-blocked copy streams one contiguous span per workgroup (each k
+  // row of the plain layout gives this tile only 256 bytes: DRAM page hits are rare)
+  const int64_t qst = a.qs_blocked ? LT : ldq;
+  const double* qp = a.qs_blocked ? a.Qs + (int64_t)blockIdx.y * n * LT + fr : a.Qs + i0 + fr;
   const double* wp = W + s0 + fr;
   // K split over gridDim.z workgroups (z-th chunk of 16-row multiples)
   const int KS = gridDim.z, z = blockIdx.z;
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(256) void k_admm_step(AdmmStep a, const double* __r
       const bool kin = k < kend;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        av[u][t] = (kin && iin[t]) ? qp[k * ldq + 16 * t] : 0.0;
+        av[u][t] = (kin && iin[t]) ? qp[k * qst + 16 * t] : 0.0;
         bv[u][t] = (kin && sin_[t]) ? wp[k * lds + 16 * t] : 0.0;
       }
     }
@@ -396,6 +400,14 @@ extern "C" int ipm_lasso_loss(ipm_handle* h, const ipm_lasso_args* a, int absm, 
   return IPM_OK;
 }
 
+__global__ void k_block_qs(int64_t n, const double* __restrict__ Qs, int64_t ldq, double* __restrict__ Qb) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;   // destination index
+  const int64_t nt = (n + LT - 1) / LT;
+  if (e >= nt * n * LT) return;
+  const int64_t il = e % LT, k = (e / LT) % n, it = e / (LT * n), i = it * LT + il;
+  Qb[e] = i < n ? Qs[k * ldq + i] : 0.0;
+}
+
 // K split of the iteration GEMM: enough workgroups for the chip (>= ~512), chunks of >= 128 rows
 static int admm_ksplit(int64_t n, int64_t S) {
   const int64_t tiles = ((S + LT - 1) / LT) * ((n + LT - 1) / LT);
@@ -412,6 +424,16 @@ extern "C" int64_t ipm_lasso_partial_doubles(int64_t n, int64_t S) {
   const int64_t tiles = ((S + LT - 1) / LT) * ((n + LT - 1) / LT);
   const int ks = admm_ksplit(n, S);
   return 4 * tiles + 8 + (ks > 1 ? tiles * ks * LT * LT + tiles : 0);
+}
+
+extern "C" int64_t ipm_lasso_qb_doubles(int64_t n) { return n > 0 ? ((n + LT - 1) / LT) * LT * n : 0; }
+
+extern "C" int ipm_lasso_block_qs(ipm_handle* h, int64_t n, const double* Qs, int64_t ldq, double* Qb) {
+  if (!h || n <= 0 || ldq < n || !Qs || !Qb) return IPM_INVALID_ARG;
+  const int64_t tot = ipm_lasso_qb_doubles(n);
+  hipLaunchKernelGGL(k_block_qs, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, h->stream, n, Qs, ldq, Qb);
+  HIPCHK(h, hipGetLastError());
+  return IPM_OK;
 }
 
 extern "C" int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* iters) {
@@ -441,6 +463,7 @@ extern "C" int ipm_lasso_admm(ipm_handle* h, const ipm_lasso_args* a, int32_t* i
   s.positive = a->positive;
   s.add_bias = a->add_bias;
   s.dual_form = a->dual_form;
+  s.qs_blocked = a->qs_blocked;
   const int ks = admm_ksplit(a->n, a->S);
   const dim3 grid((unsigned)((a->S + LT - 1) / LT), (unsigned)((a->n + LT - 1) / LT), (unsigned)ks);
   const int64_t nblk = (int64_t)grid.x * grid.y;

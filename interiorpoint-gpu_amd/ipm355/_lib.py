@@ -108,6 +108,8 @@ EXPORTS = {
     "ipm_lasso_loss": (C.c_int, [P, P, C.c_int, P, P]),
     "ipm_lasso_partial_doubles": (I64, [I64, I64]),
     "ipm_lasso_admm": (C.c_int, [P, P, C.POINTER(C.c_int32)]),
+    "ipm_lasso_qb_doubles": (I64, [I64]),
+    "ipm_lasso_block_qs": (C.c_int, [P, I64, P, I64, P]),
 }
 
 _lib = None

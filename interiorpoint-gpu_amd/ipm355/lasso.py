@@ -42,7 +42,7 @@ class LassoArgs(C.Structure):
                 ("dual_form", L.I32), ("compute_loss", L.I32),
                 ("ba_bcast", L.I32), ("eta_bcast", L.I32), ("b_bcast", L.I32), ("reg_bcast", L.I32),
                 ("AT", L.P), ("ldat", L.I64), ("b", L.P), ("ldb", L.I64), ("reg", L.P), ("R", L.P),
-                ("gaps", L.P), ("ldg", L.I64), ("gap_cols", L.P)]
+                ("gaps", L.P), ("ldg", L.I64), ("gap_cols", L.P), ("qs_blocked", L.I32)]
 
 
 def _dev(a, dev):
@@ -117,8 +117,8 @@ class LassoSolver:
             self.bA_cache = self._bA(self._b_dev)
             # Qinv_cache *= -m * rho (LassoSolver.py:220): in place on the transpose, which is all
             # the iteration reads
-            self.Qs = self.QinvT
-            h.check(lib.ipm_lasso_scale(h.ptr, n, n, L.dptr(self.Qs), n, -self.m * self.rho, 1.0, 0), h.ptr)
+            h.check(lib.ipm_lasso_scale(h.ptr, n, n, L.dptr(self.QinvT), n, -self.m * self.rho, 1.0, 0), h.ptr)
+            self.Qs = self._blocked(self.QinvT)
         else:
             self.solve_func = self._run_admm_chunks
 
@@ -134,6 +134,15 @@ class LassoSolver:
         h.check(self.lib.ipm_gemm_tn(h.ptr, n, Sb, n, 1.0, L.dptr(self.QinvT), n, L.dptr(AtB), Sb, 0.0,
                                      L.dptr(bA), Sb), h.ptr)
         return bA
+
+    def _blocked(self, Qs):
+        """The ADMM step's tile-blocked copy of Qs (ipm_lasso_block_qs): each workgroup of the
+        iteration GEMM then streams one contiguous span of it."""
+        import torch
+        n = self.n
+        Qb = torch.empty(int(self.lib.ipm_lasso_qb_doubles(n)), dtype=torch.float64, device=self.dev)
+        self.h.check(self.lib.ipm_lasso_block_qs(self.h.ptr, n, L.dptr(Qs), n, L.dptr(Qb)), self.h.ptr)
+        return Qb
 
     def _loss_buffers(self, S):
         import torch
@@ -155,7 +164,7 @@ class LassoSolver:
                   eta=_dev(np.atleast_1d(eta), self.dev), reg=_dev(np.atleast_1d(reg), self.dev))
         a = LassoArgs()
         a.n, a.S, a.m, a.lds = self.n, S, self.m, S
-        a.Qs, a.ldq = L.dptr(Qs), self.n
+        a.Qs, a.ldq, a.qs_blocked = L.dptr(Qs), self.n, 1   # Qs: the tile-blocked copy (_blocked)
         a.bA, a.ldba, a.ba_bcast = L.dptr(bA), int(bA.shape[1]), int(bA.shape[1] == 1 and S > 1)
         a.eta, a.eta_bcast = L.dptr(st["eta"]), int(st["eta"].numel() == 1 and S > 1)
         for k in ("x", "alpha", "u", "W0", "W1", "partial"):
@@ -220,6 +229,7 @@ class LassoSolver:
         # Qinv_cache * -self.m * self.rho, left to right (LassoSolver.py:386)
         self.h.check(self.lib.ipm_lasso_scale(self.h.ptr, n, n, L.dptr(Qs), n, float(-self.m), float(self.rho), 1),
                      self.h.ptr)
+        Qs = self._blocked(Qs)
         gaps_dev = torch.zeros((self.max_iters, self.num_samples), dtype=torch.float64, device=self.dev) \
             if self.compute_loss else None
         indices = np.array(range(self.b.shape[1]))

@@ -59,7 +59,9 @@ def test_oracle_matches_reference(name):
 def test_lasso_args_layout():
     from ipm355.lasso import LassoArgs
     # 4 int64 + (ptr, int64, ptr, int64, ptr) + 6 ptr + 4 double + 10 int32 + 9 pointer/int64 fields
-    assert ctypes.sizeof(LassoArgs) == 32 + 40 + 48 + 32 + 40 + 72
+    # + qs_blocked (int32, padded to the struct's 8-byte alignment)
+    assert ctypes.sizeof(LassoArgs) == 32 + 40 + 48 + 32 + 40 + 72 + 8
+    assert LassoArgs.qs_blocked.offset == 32 + 40 + 48 + 32 + 40 + 72
 
 
 @pytest.mark.gpu
