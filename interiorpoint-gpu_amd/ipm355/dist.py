@@ -72,7 +72,7 @@ def gather_results(local: dict, n_instances: int, device=None, xs: dict | None =
         if xs is not None:
             tab[k, FIELDS:] = torch.as_tensor(np.asarray(xs[idx], dtype=np.float64))
     tab = tab.to(_table_device(device))
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():   # (world 1 too: a one-rank RCCL group runs the same device gather)
         parts = [torch.empty_like(tab) for _ in range(world)]
         dist.all_gather(parts, tab)
         allt = torch.cat(parts).cpu().numpy()

@@ -39,13 +39,19 @@ def instance(seed):
 
 if __name__ == "__main__":
     out_dir = sys.argv[1]
-    seeds = list(range(1000, 1008))
+    backend = sys.argv[2] if len(sys.argv) > 2 else "gloo"   # "nccl": RCCL (one rank per GPU)
+    seeds = list(range(1000, 1008)) if len(sys.argv) <= 3 else list(range(1000, 1000 + int(sys.argv[3])))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
     try:
         tab, X = D.solve_sharded(lambda i: instance(seeds[i]), len(seeds), QPSolver, device=0, gather_x=True)
         rank = dist.get_rank()
         np.save(os.path.join(out_dir, f"tab{rank}.npy"), tab)
         np.save(os.path.join(out_dir, f"x{rank}.npy"), X)
+        with open(os.path.join(out_dir, f"backend{rank}.txt"), "w") as f:
+            f.write(dist.get_backend())
     finally:
         dist.destroy_process_group()

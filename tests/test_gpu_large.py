@@ -246,6 +246,29 @@ def test_sharded_two_ranks_real_solvers(tmp_path):
     np.testing.assert_array_equal(np.load(tmp_path / "x0.npy"), np.load(tmp_path / "x1.npy"))
 
 
+def test_sharded_rccl_one_rank(tmp_path):
+    """The RCCL branch of the sharded path (backend "nccl": the gather table lives on the rank's
+    GPU and goes through a device all_gather), as far as a one-GPU box allows: ONE rank in an RCCL
+    process group (RCCL refuses two ranks on one device), solve_sharded with the device QPSolver on
+    two M4 reference fixtures, the table + x* through the RCCL all_gather, checked against them."""
+    import sys
+    from ipm355 import dist
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
+    rc = dist.launch_local(1, [sys.executable, "-u", worker, str(tmp_path), "nccl", "2"])
+    assert rc == 0
+    assert (tmp_path / "backend0.txt").read_text() == "nccl"
+    tab = np.load(tmp_path / "tab0.npy")
+    X = np.load(tmp_path / "x0.npy")
+    for i in range(2):
+        z = _fixture(f"m4_qp_{1000 + i}")
+        err = rel(X[i], z["xstar"])
+        ref_iters = int(sum(z["inner_iters"]) + sum(z["phase1_inner_iters"]))
+        print(f"[rccl m4_qp_{1000 + i}] x* rel {err:.2e}, iters {int(tab[i, 1])} vs {ref_iters}")
+        assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"])), (i, err)
+        if bool(z["sens_steps_stable"]):
+            assert int(tab[i, 1]) == ref_iters
+
+
 @pytest.mark.parametrize("name", ["m3_qp_full", "m3_lp_full"])
 def test_m3_full_solve(name):
     """The headline instance solved to COMPLETION: M3-QP n=8192, m=2048, test_QP
