@@ -1860,6 +1860,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   // IPM_SPLIT=0: no K-split trailing tiles (read per call: tests compare both)
   const char* esp = getenv("IPM_SPLIT");
   const bool split_on = !(esp && esp[0] == '0');
+  // IPM_LAZYC=0: no lazy-C trailing tiles (read per call: tests compare both)
+  const char* elz = getenv("IPM_LAZYC");
+  const bool lazy_on = !(elz && elz[0] == '0');
   PairPlan pl = potrf_pair_plan(n, ncols, nblocks, defer);
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     const int kind = pl.kind[bk];
@@ -2056,7 +2059,12 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     // IPM_ROWPOS=1: the non-critical row chunks among the trailing tiles (row_slots)
     static const bool rowpos_on = [] { const char* e = getenv("IPM_ROWPOS"); return e && e[0] == '1'; }();
     b.sa = b.sb = b.ns;
-    if (b.s_full > 0 && !defer && (split_on || rowpos_on)) {
+    // a plain launch whose trailing tiles can all run the lazy-C loop keeps them whole: the lazy
+    // kernel gains more than the K-halves of the last round (r3: 6.20 -> 6.12-6.16 ms at n = 8192)
+    static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
+    const bool lazy_cand = lazy_on && fasts_on && vec && b.s.K == CH_NB && b.nstrip == 0 && (b.s.ni % 128) == 0;
+    const bool split_here = split_on && !lazy_cand;
+    if (b.s_full > 0 && !defer && (split_here || rowpos_on)) {
       // the planner's split count and row positions (cached per size and block: they depend on
       // nothing else)
       struct Plan { int64_t q = -1, sa = 0, sb = 0; };
@@ -2068,7 +2076,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       Plan p;
       {
         std::lock_guard<std::mutex> lk(mu);
-        auto& v = cache[{n, ncols, (split_on ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0)}];
+        auto& v = cache[{n, ncols, (split_on ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0) | (lazy_on ? 4 : 0)}];
         if ((int64_t)v.size() < nblocks) v.assign(nblocks, Plan{});
         if (v[bk].q < 0) {
           Plan& w = v[bk];
@@ -2078,7 +2086,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
             static const double tb = [] { const char* e = getenv("IPM_ROW_TB"); return e ? atof(e) : 1.35; }();
             row_slots(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.nstrip, b.ns, tc, lac, nra_h, ta, tb, w.sa, w.sb);
           }
-          w.q = split_on ? plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, nra_h + b.nrb,
+          w.q = split_here ? plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, nra_h + b.nrb,
                                       potrf_split_cap(n), tc, b.nstrip, lac, nra_h, w.sa, w.sb)
                          : 0;
           static const bool dbg = getenv("IPM_SPLIT_DEBUG") != nullptr;
@@ -2095,7 +2103,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       static const bool rpad_on = [] { const char* e = getenv("IPM_ROWPAD"); return !(e && e[0] == '0'); }();
       if (rpad_on && b.sa < b.ns) b.rpad_a = (8 - (b.nra - nchd_h) % 8) % 8;
       if (rpad_on && b.sb < b.ns) b.rpad_b = (8 - b.nrb % 8) % 8;
-      if (split_on) {
+      if (split_here) {
         b.sscr = ws + potrf_split_scratch_off(n);
         b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
       }
@@ -2133,10 +2141,8 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
                          b.rpad_a + b.rpad_b;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
-    static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
     // (r3 A/B, two pairs: 6.48 / 6.52 -> 6.41 / 6.44 ms at the bordered n = 8193; IPM_LAZYC=0: off)
-    static const bool lazy_on = [] { const char* e = getenv("IPM_LAZYC"); return !(e && e[0] == '0'); }();
     const bool lazy = lazy_on && fasts && b.s.K == CH_NB && b.nstrip == 0 && b.s_full == b.ns;
     if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
@@ -2946,9 +2952,11 @@ __global__ void k_copy_rows(int64_t rows, int64_t cols, const double* __restrict
   const int64_t r = e / cols, c = e - r * cols;
   out[r * ldo + c] = in[r * ldi + c];
 }
+// workspace: the inverted diagonal blocks and their transposes, ONE 128-row panel of L transposed
+// for the backward GEMMs (128 n doubles, not a transposed copy of all of L), the diag staging
 int64_t potrs_blocked_ws_doubles(int64_t n, int64_t nrhs) {
   const int64_t nblk = cdiv(n, 128);
-  return 2 * nblk * 16384 + n * n + 128 * nrhs + 64;
+  return 2 * nblk * 16384 + 128 * n + 128 * nrhs + 64;
 }
 void potrs_blocked(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B, int64_t ldb,
                    double* ws) {
@@ -2956,11 +2964,10 @@ void potrs_blocked(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int
   const int64_t nblk = cdiv(n, 128);
   double* Xs = ws;
   double* XsT = Xs + nblk * 16384;
-  double* Lr = XsT + nblk * 16384;
-  double* T = Lr + n * n;
+  double* Lp = XsT + nblk * 16384;   // Lp[k * n + c] = L(j0 + k, c), c < j0: block row j, transposed
+  double* T = Lp + 128 * n;
   hipLaunchKernelGGL(k_trinv128, dim3((unsigned)nblk), dim3(512), 0, st, n, L, ldl, Xs);
   hipLaunchKernelGGL(k_block_transpose128, dim3((unsigned)cdiv(nblk * 16384, 256)), dim3(256), 0, st, nblk, Xs, XsT);
-  transpose(st, n, n, L, ldl, Lr, n);   // Lr[r * n + c] = L(r, c)
   auto gemm = [&](int64_t ni, int64_t nj, int64_t K, const double* X, int64_t ldx, const double* Y, int64_t ldy,
                   double* C, int64_t ldc, bool sub) {
     if (ni <= 0 || nj <= 0 || K <= 0) return;
@@ -2991,7 +2998,10 @@ void potrs_blocked(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int
   for (int64_t j = nblk - 1; j >= 0; --j) {
     const int64_t j0 = j * 128, j1 = std::min<int64_t>(n, j0 + 128);
     diag(j, XsT + j * 16384);
-    gemm(nrhs, j0, j1 - j0, B + j0 * ldb, ldb, Lr + j0 * n, n, B, ldb, true);
+    if (j0 > 0) {
+      transpose(st, j0, j1 - j0, L + j0, ldl, Lp, n);   // (the panel the GEMM below reads)
+      gemm(nrhs, j0, j1 - j0, B + j0 * ldb, ldb, Lp, n, B, ldb, true);
+    }
   }
 }
 

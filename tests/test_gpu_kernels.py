@@ -155,26 +155,29 @@ def test_potrf_ragged_rows(n, ncols, monkeypatch):
 @pytest.mark.parametrize("n,ncols", [(8194, 8193), (4100, 4100)])
 def test_potrf_split_trailing_tiles(n, ncols, monkeypatch):
     """Trailing tiles of a launch's last round split in two K halves (IPM_SPLIT, default on; the
-    upper half's partial tile handed over through the workspace): the factor agrees with the
-    unsplit one to fp64 rounding and with torch's Cholesky to 1e-10."""
+    upper half's partial tile handed over through the workspace), on the C-burst tile loop
+    (IPM_LAZYC=0: the default keeps lazy-eligible launches whole), and the lazy-C default: the
+    factors agree with the unsplit one to fp64 rounding and with torch's Cholesky to 1e-10."""
     import torch
     from gpu_util import potrf as P
     g = torch.Generator(device="cuda").manual_seed(n + 1)
     M = torch.rand((n + 5, n), dtype=torch.float64, device="cuda", generator=g) - 0.5
     A = M.T @ M + n * torch.eye(n, dtype=torch.float64, device="cuda")
     out = {}
-    for mode in ("0", "1"):
+    for mode, lazy in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("IPM_SPLIT", mode)
+        monkeypatch.setenv("IPM_LAZYC", lazy)
         H = A.clone()
         rc, info = P(H, n, n, ncols=ncols)
         assert rc == 0 and info == 0
-        out[mode] = torch.tril(H.T)[:, :ncols]
-    scale = out["0"].abs().max()
-    d = ((out["1"] - out["0"]).abs().max() / scale).item()
-    print(f"n={n}: split vs unsplit max rel {d:.2e}")
-    assert d < 1e-12
+        out[mode + lazy] = torch.tril(H.T)[:, :ncols]
+    scale = out["00"].abs().max()
     L11 = torch.linalg.cholesky(A[:ncols, :ncols])
-    assert ((out["1"][:ncols] - L11).abs().max() / L11.abs().max()).item() < 1e-10
+    for k in ("10", "11"):
+        d = ((out[k] - out["00"]).abs().max() / scale).item()
+        print(f"n={n}: split {k[0]} lazy {k[1]} vs unsplit max rel {d:.2e}")
+        assert d < 1e-12
+        assert ((out[k][:ncols] - L11).abs().max() / L11.abs().max()).item() < 1e-10
 
 
 @pytest.mark.parametrize("n", [1, 7, 64, 65, 200, 1030, 2100])
