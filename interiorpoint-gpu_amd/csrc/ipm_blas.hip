@@ -1270,7 +1270,7 @@ struct RoleTrace {
 // LAZY (default; IPM_LAZYC=0 turns it off.  FASTS launches whose trailing tiles are all whole K = 256 tiles, no strips or
 // K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
 // before the first MFMA
-template <bool VEC, bool FASTS = false, bool LAZY = false>
+template <bool VEC, bool FASTS = false, int LAZY = 0>
 __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ BlockSmem sm;
   __shared__ int sticket, sflag;
@@ -1662,7 +1662,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         }
         // (both loops in one kernel raised the SGPR spills 89 -> 621 and cost 2.5 %: the launch
         // picks the kernel instead, FASTS)
-        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0, LAZY && FASTS && VEC>(
+        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0, (FASTS && VEC) ? LAZY : 0>(
             g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
                      : b.f0 + (u < 0 ? st : b.s_full + p),
             sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
@@ -1863,6 +1863,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   // IPM_LAZYC=0: no lazy-C trailing tiles (read per call: tests compare both)
   const char* elz = getenv("IPM_LAZYC");
   const bool lazy_on = !(elz && elz[0] == '0');
+  const bool lazy2_on = lazy_on && !(elz && elz[0] == '1');   // IPM_LAZYC=1: K = 256 tiles only
   PairPlan pl = potrf_pair_plan(n, ncols, nblocks, defer);
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     const int kind = pl.kind[bk];
@@ -2062,7 +2063,9 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     // a plain launch whose trailing tiles can all run the lazy-C loop keeps them whole: the lazy
     // kernel gains more than the K-halves of the last round (r3: 6.20 -> 6.12-6.16 ms at n = 8192)
     static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
-    const bool lazy_cand = lazy_on && fasts_on && vec && b.s.K == CH_NB && b.nstrip == 0 && (b.s.ni % 128) == 0;
+    // (LAZY 2: the block pairs' K = 512 tiles, strips included)
+    const bool lazy_cand = lazy_on && fasts_on && vec && (b.s.ni % 128) == 0 &&
+                           ((b.s.K == CH_NB && b.nstrip == 0) || (lazy2_on && b.s.K == 2 * CH_NB));
     const bool split_here = split_on && !lazy_cand;
     if (b.s_full > 0 && !defer && (split_here || rowpos_on)) {
       // the planner's split count and row positions (cached per size and block: they depend on
@@ -2144,7 +2147,10 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
     // (r3 A/B, two pairs: 6.48 / 6.52 -> 6.41 / 6.44 ms at the bordered n = 8193; IPM_LAZYC=0: off)
     const bool lazy = lazy_on && fasts && b.s.K == CH_NB && b.nstrip == 0 && b.s_full == b.ns;
-    if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    const bool lazy2 = lazy2_on && fasts && b.s.K == 2 * CH_NB && b.nstrip + b.s_full == b.ns &&
+                       (b.nstrip == 0 || b.s2.K == 2 * CH_NB) && (b.nrag == 0 || b.rag_K <= 2 * CH_NB);
+    if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, 1>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    else if (vec && lazy2) hipLaunchKernelGGL((k_potrf_block<true, true, 2>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec) hipLaunchKernelGGL((k_potrf_block<true, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else hipLaunchKernelGGL((k_potrf_block<false, false>), dim3((unsigned)grid), dim3(256), 0, st, b);

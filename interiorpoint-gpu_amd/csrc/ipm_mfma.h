@@ -126,7 +126,7 @@ struct alignas(16) MfSmem {
 // is spread over the K loop instead of a burst before the first MFMA (all workgroups of a round
 // start together: the burst is bandwidth-bound).  C + sum(products) in another association order.
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false, bool SPLITADD = false,
-          int LOOP = 0, bool LAZYC = false, bool CST = false>
+          int LOOP = 0, int LAZYC = 0, bool CST = false>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
                                           double* part = nullptr, unsigned* pflag = nullptr, int64_t kb = -1,
                                           int64_t ke = -1) {
@@ -277,8 +277,9 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   // and the sign are applied when the slab goes to LDS.  tools/gemm_lab.hip (lab2): +6-9 %.
   static_assert(LOOP == 0 || (BM_ == 128 && VEC && WJ == 2), "fast loop: 128-tiles, vector loads");
   if constexpr (LAZYC) {
-    // exactly 16 slabs (K = 256: the Cholesky's trailing tiles; the caller guarantees it), fully
-    // unrolled: accumulator block q = s is read in slab s and added in slab s + 2
+    // exactly 16 LAZYC slabs (K = 256 or, LAZYC 2, the block pairs' K = 512: the Cholesky's
+    // trailing tiles; the caller guarantees it), fully unrolled: accumulator block q is read in
+    // slab q LAZYC and added in slab (q + 2) LAZYC
     double fx[PT], fy[PT];
     auto fload = [&](int64_t s) {
       const double2* xs = reinterpret_cast<const double2*>(xp + s * xstep);
@@ -308,8 +309,8 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
       for (int r = 0; r < 4; ++r) v[r] = a.C[(j0 + 4 * r) * a.ldc + i];
       return v;
     };
-    constexpr int NS = 16;
-    static_assert(TWJ * TWI == NS, "one accumulator block per slab");
+    constexpr int NS = 16, R = LAZYC > 0 ? LAZYC : 1, NSL = NS * R;
+    static_assert(TWJ * TWI == NS, "one accumulator block per R slabs");
     dbl4 cq[NS];
     fload(0);
     fstore(0);
@@ -317,14 +318,17 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     cq[0] = cload(0);
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < NSL; ++s) {
       const int buf = s & 1;
       const double* bx = sX[buf];
       const double* by = sY[buf];
       fstore(buf ^ 1);
-      fload(s + 2 < NS ? s + 2 : NS - 1);
-      if (s + 1 < NS) cq[s + 1] = cload(s + 1);
-      if (s >= 2) acc[(s - 2) / TWI][(s - 2) % TWI] += cq[s - 2];
+      fload(s + 2 < NSL ? s + 2 : NSL - 1);
+      if (s % R == 0) {
+        const int q = s / R;
+        if (q + 1 < NS) cq[q + 1] = cload(q + 1);
+        if (q >= 2) acc[(q - 2) / TWI][(q - 2) % TWI] += cq[q - 2];
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kk = 0; kk < BK / 4; ++kk) {
