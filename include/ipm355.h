@@ -139,6 +139,9 @@ typedef struct ipm_newton_result {
   int64_t backtracks;   /* total trial points examined                           */
   int64_t ls_compared;  /* IPM_LS_COMPARE: steps compared / steps whose table and  */
   int64_t ls_flips;     /*   exact step sizes differ                             */
+  int64_t linalg_error; /* the solve ended on a LinAlgError: a least-squares      */
+                        /*   eigensolve did not converge (the reference's try /   */
+                        /*   except in NewtonSolver.py:148-155 returns a failure)  */
 } ipm_newton_result;
 
 /* ---- handle --------------------------------------------------------------- */
@@ -219,11 +222,21 @@ int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda
    averages (ms) over the Newton iterations since the reset, and their count */
 int ipm_set_timing(ipm_handle* h, int on);
 int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms, double* count);
-/* debug knob: the spin bound (in s_sleep(1) units) after which the persistent backward solve's
-   chain step stops waiting for its producer and raises its device error word; the Newton step's
-   readback then returns IPM_HIP_ERROR instead of using the step.  0 restores the default 2^20.
-   Process-wide; tests use a tiny bound to trip the error path once. */
+/* debug knob: the wall-clock bound (microseconds, s_memrealtime) after which the persistent
+   backward solve's chain step stops waiting for its producer and raises its device error word; the
+   Newton step's readback then returns IPM_HIP_ERROR instead of using the step.  0 restores the
+   default 1 s.  Process-wide; tests use a tiny bound to trip the error path once. */
 int ipm_debug_set_trsv_spin_limit(unsigned limit);
+/* debug knob: the same wall-clock bound (microseconds; 0 = default 1 s) for every wait of the
+   ticketed Cholesky (k_potrf_block: row chunks on their diagonal role, look-ahead / fold / split
+   hand-offs, trailing tiles kept off critical CUs).  A wait that runs out sets info to -1000
+   (IPM_INFO_SPIN: never a LAPACK column), every later launch of the factorization returns at once,
+   and ipm_potrf / the Newton step return IPM_HIP_ERROR.  Process-wide. */
+int ipm_debug_set_potrf_spin_limit(unsigned microseconds);
+/* debug knob: the k-th least-squares eigensolve from now (k = 0: the next one) reports
+   non-convergence whatever happened (-1: off).  Tests that one failed eigensolve among several in
+   a Newton step is not overwritten by a later converged one. */
+int ipm_debug_lstsq_fail_call(int k);
 /* debug knob: the backward-solve workgroup holding chain ticket `ticket` sleeps ~7 ms before
    publishing its progress word (-1: off), so later tickets overtake it -- exercises the monotonic
    progress publish.  Process-wide. */

@@ -265,6 +265,24 @@ void gemm_nt_sub(hipStream_t st, int64_t m, int64_t n, int64_t k, const double* 
   gemm_nt_sub_launch(st, m, n, k, A, lda, B, ldb, C, ldc, nullptr);
 }
 
+void gemm_kk(hipStream_t st, int64_t ni, int64_t nj, int64_t k, const double* X, int64_t ldx, const double* Y,
+             int64_t ldy, double* C, int64_t ldc) {
+  if (ni <= 0 || nj <= 0) return;
+  GemmArgs a;
+  a.ni = ni;
+  a.nj = nj;
+  a.K = k;
+  a.X = X;
+  a.ldx = ldx;
+  a.Y = Y;
+  a.ldy = ldy;
+  a.C = C;
+  a.ldc = ldc;
+  a.alpha = 1.0;
+  a.beta = 0.0;
+  mfma_gemm_launch(st, a);
+}
+
 // =====================================================================================
 // Cholesky panel (width nb <= 128) in two launches, no redundant work:
 //   k_potrf_diag : ONE workgroup factors the nb x nb diagonal block in LDS (16 x 16 blocks,
@@ -892,6 +910,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   if (fail) {
     if (tid == 0) {
       atomicCAS(info, 0, (int)(k0 + fail));
+      __threadfence();   // (info before the failure word: a waiter released by failw cannot report first)
       if (failw) atomicCAS(failw, 0u, (unsigned)(k0 + fail));
       // release the row workgroups (they finish on garbage; the failed factor is discarded)
       if (pubL) {
@@ -920,6 +939,19 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 }
 #undef STAMP
 
+// control words of one Cholesky launch (k_potrf_block; the header of block_ctl_words)
+enum {
+  CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
+  CTL_NF = 9,                         // next-diagonal-block fold tiles done
+  // critical-path roles (P(a) diagonal, the row chunks P(b) needs, the NF tiles, P(b) diagonal):
+  // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
+  // by a workgroup that landed on that CU
+  CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
+  CTL_XQ = CTL_SPILL + NCRIT,         // trailing-tile queue counter of each XCD (8 words)
+  CTL_FLEX_S = CTL_XQ + 8, CTL_FLEX_R,  // flexible tickets: trailing tiles / row chunks taken
+  CTL_HDR = CTL_FLEX_R + 1
+};
+
 // Row role: rows below the diagonal block, L21 = A21 L11^-T, 64 rows per workgroup, 16 rows per
 // wave.  Each wave runs the 8-step block forward substitution in MFMA registers,
 //   X_J = (B_J - sum_{P<J} X_P L_JP^T) Dinv_J^T,
@@ -934,7 +966,8 @@ template <bool FUSED = false>
 __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, int nb, double* __restrict__ A,
                                          int64_t lda, const double* dinv, const double* pubL,
                                          unsigned* progress, int next_nb, unsigned* nextc, double* stage,
-                                         int* sflag, unsigned* done = nullptr, bool fold_pub = true) {
+                                         int* sflag, unsigned* done = nullptr, bool fold_pub = true,
+                                         int* sinfo = nullptr, unsigned* failw = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int64_t row = k0 + nb + chunk * PF_RB + wv * 16 + fr;
@@ -955,6 +988,10 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
 #pragma unroll
   for (int J = 0; J < 8; ++J) {
     if (16 * J >= nb) break;   // a partial panel's diagonal role stops at its last block column
+    // (every lane polls.  No bound of its own -- a wall-clock start held across this loop made the
+    // kernel spill registers: the diagonal role it waits for is resident (lower ticket), its only
+    // waits are the bounded ones at its start, and after them it always publishes: progress
+    // reaches every block row, or 0xFFFFFFFF when the block fails)
     while (known <= (unsigned)J) {
       known = ld_ctl(progress);
       if (known <= (unsigned)J) __builtin_amdgcn_s_sleep(2);
@@ -1010,10 +1047,11 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
   // (nb == 128 here).  The second factor is this panel's result for the first nchd row chunks.
   if (tid == 0) {
     int ok = 1;
-    while (ld_ctl(nextc) < (unsigned)nchd) {
-      if (ld_ctl(progress) == 0xFFFFFFFFu) { ok = 0; break; }   // diagonal failed: info is set
-      __builtin_amdgcn_s_sleep(2);
-    }
+    spin_until<2>(sinfo, failw, [&] {
+      if (ld_ctl(nextc) >= (unsigned)nchd) return true;
+      if (ld_ctl(progress) == 0xFFFFFFFFu) { ok = 0; return true; }   // diagonal failed: info is set
+      return false;
+    });
     *sflag = ok;
   }
   __syncthreads();
@@ -1188,17 +1226,6 @@ struct BlockArgs {
 #ifndef FLEX_PROG
 #define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
 #endif
-enum {
-  CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
-  CTL_NF = 9,                         // next-diagonal-block fold tiles done
-  // critical-path roles (P(a) diagonal, the row chunks P(b) needs, the NF tiles, P(b) diagonal):
-  // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
-  // by a workgroup that landed on that CU
-  CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
-  CTL_XQ = CTL_SPILL + NCRIT,         // trailing-tile queue counter of each XCD (8 words)
-  CTL_FLEX_S = CTL_XQ + 8, CTL_FLEX_R,  // flexible tickets: trailing tiles / row chunks taken
-  CTL_HDR = CTL_FLEX_R + 1
-};
 
 // Trailing tiles by XCD (s_map 2): the tri tile list is cut into 8 contiguous runs; a workgroup
 // takes the next tile of ITS XCD's run (HW_REG_XCC_ID); an exhausted run sends it on to the next
@@ -1233,11 +1260,12 @@ union BlockSmem {
   MfSmem<32, 2> g32;
 };
 
-// thread 0 waits until words w[0..cnt) are all >= target; then the workgroup proceeds
-__device__ __forceinline__ void wait_words(unsigned* w, int cnt, unsigned target) {
+// thread 0 waits until words w[0..cnt) are all >= target (or the bound runs out); then the
+// workgroup proceeds
+__device__ __forceinline__ void wait_words(unsigned* w, int cnt, unsigned target, int* info, unsigned* failw) {
   if (threadIdx.x == 0)
     for (int i = 0; i < cnt; ++i)
-      while (ld_ctl(w + i) < target) __builtin_amdgcn_s_sleep(2);
+      if (!spin_until<2>(info, failw, [&] { return ld_ctl(w + i) >= target; })) break;
   __syncthreads();
 }
 
@@ -1276,6 +1304,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ int sticket, sflag;
   const int tid = threadIdx.x;
   if (tid == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
+  unsigned* const failw = &b.ctl[CTL_FAIL];
   __syncthreads();
   int64_t t = sticket;
 #ifdef IPM_ROLE_TRACE
@@ -1339,7 +1368,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
           tgt = 0;
           for (int64_t i = 2 * q; i < 2 * q + 2 && i < b.la32_T; ++i) tgt += (unsigned)(i + 1);
         }
-        while (ld_ctl(la_done + q) < tgt) __builtin_amdgcn_s_sleep(2);
+        if (!spin_until<2>(b.info, failw, [&] { return ld_ctl(la_done + q) >= tgt; })) break;
       }
     __syncthreads();
   };
@@ -1455,7 +1484,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   const int nbp = pb ? b.wbw : b.wa;
   if (kind == K_DIAG) {
     ROLE(pb ? 3 : 1);
-    if (pb) wait_words(&b.ctl[CTL_NF], 1, (unsigned)b.nnf);
+    if (pb) wait_words(&b.ctl[CTL_NF], 1, (unsigned)b.nnf, b.info, failw);
     else wait_la(0, b.wa - 1);
     diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
     return;
@@ -1470,13 +1499,13 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
       const int64_t r0 = b.wbw + chunk * PF_RB;
       const int64_t q1 = std::min<int64_t>((std::min<int64_t>(r0 + PF_RB, b.n - k1) - 1) / PF_RB, b.nra - 1);
-      wait_words(pa_done + r0 / PF_RB, (int)(q1 - r0 / PF_RB + 1), 1u);
+      wait_words(pa_done + r0 / PF_RB, (int)(q1 - r0 / PF_RB + 1), 1u, b.info, failw);
     } else {
       const int64_t r0 = b.wa + chunk * PF_RB;
       wait_la(r0, std::min<int64_t>(r0 + PF_RB, b.n - b.cb) - 1);
     }
     row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
-                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk], false);
+                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk], false, b.info, failw);
     return;
   }
   if (kind == K_NF) {
@@ -1487,10 +1516,10 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     while (q > ti) { q -= ti + 1; ++ti; }   // t -> (ti, tj = q), tj <= ti
     const int tj = q;
     (void)T;
-    if (tid == 0) {
-      while (ld_ctl(&b.ctl[CTL_PA_NEXT]) < (unsigned)nchd && ld_ctl(&b.ctl[CTL_PA_PROG]) != 0xFFFFFFFFu)
-        __builtin_amdgcn_s_sleep(2);
-    }
+    if (tid == 0)
+      spin_until<2>(b.info, failw, [&] {
+        return ld_ctl(&b.ctl[CTL_PA_NEXT]) >= (unsigned)nchd || ld_ctl(&b.ctl[CTL_PA_PROG]) == 0xFFFFFFFFu;
+      });
     __syncthreads();
     const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, fk = lane >> 4;
     const int ib = 32 * ti + 16 * (wv & 1), jb = 32 * tj + 16 * (wv >> 1);
@@ -1534,12 +1563,11 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     // never beside a critical-path role: wait (holding the slot) until none runs on this CU
     if (tid == 0) {
       const unsigned me = 1u + cu_key();
-      for (;;) {
+      spin_until<20>(b.info, failw, [&] {
         bool busy = false;
         for (int i = 0; i < NCRIT; ++i) busy |= ld_ctl(&b.ctl[CTL_CRIT + i]) == me;
-        if (!busy) break;
-        __builtin_amdgcn_s_sleep(20);
-      }
+        return !busy;
+      });
     }
     __syncthreads();
     // G(:, block J) (+)= C_s^T diag(w_s) C_s over this job's k rows (64 x 64 tiles, rows >= 256 J)
@@ -1623,7 +1651,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       if (q >= 0) {
         ROLE(7);
         __hip_atomic_store(&b.ctl[CTL_SPILL + q], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (ld_ctl(&b.ctl[CTL_CRIT + q]) == me) __builtin_amdgcn_s_sleep(20);
+        spin_until<20>(b.info, failw, [&] { return ld_ctl(&b.ctl[CTL_CRIT + q]) != me; });
         sflag = (int)__hip_atomic_exchange(&b.ctl[CTL_SPILL + q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         sflag = (int)(t + 1);
@@ -1665,7 +1693,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0, (FASTS && VEC) ? LAZY : 0>(
             g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
                      : b.f0 + (u < 0 ? st : b.s_full + p),
-            sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p);
+            sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p, -1, -1, b.info, failw);
       }
     }
   }
@@ -1840,6 +1868,26 @@ static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks, bool 
   }
   return pl;
 }
+
+// wall-clock bounds of the device-side waits: microseconds -> ticks of
+// s_memrealtime (hipDeviceAttributeWallClockRate, kHz; 100 MHz on MI355X)
+static unsigned long long wall_ticks(unsigned us) {
+  static long long khz = -1;
+  if (khz < 0) {
+    int dev = 0, v = 0;
+    hipGetDevice(&dev);
+    khz = (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev) == hipSuccess && v > 0) ? v : 100000;
+  }
+  const unsigned long long t = (unsigned long long)us * (unsigned long long)khz / 1000ull;
+  return t > 0 ? t : 1;
+}
+constexpr unsigned SPIN_US_DEFAULT = 1000000;   // 1 s: no legitimate wait comes near it
+// (the device global ipm_spin_ticks of the current device; its initial value is 1 s at 100 MHz)
+static void set_spin_ticks(int which, unsigned us) {
+  const unsigned long long t = wall_ticks(us ? us : SPIN_US_DEFAULT);
+  hipMemcpyToSymbol(HIP_SYMBOL(ipm_spin_ticks), &t, sizeof(t), which * sizeof(t), hipMemcpyHostToDevice);
+}
+void set_potrf_spin_limit_us(unsigned us) { set_spin_ticks(0, us); }
 
 void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
                        const DeferSyrk* ds) {
@@ -2718,8 +2766,7 @@ struct Trsv128Smem {
 __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, const double* __restrict__ L,
                                                         int64_t ldl, const double* __restrict__ b, int64_t bstride,
                                                         const double* __restrict__ Xws, double* y, unsigned* ctl,
-                                                        unsigned* err, unsigned spin_limit,
-                                                        int delay_ticket) {
+                                                        unsigned* err, int delay_ticket) {
   __shared__ Trsv128Smem sm;
   __shared__ int sticket;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;   // 8 waves
@@ -2770,9 +2817,11 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
         tv0[jj] = (cc < rows && kr < krows) ? src[0] : 0.0;
         tv1[jj] = (cc < rows && kr + 1 < krows) ? src[1] : 0.0;
       }
-      while (known <= (unsigned)tp) {
-        known = ld_ctl(&ctl[1]);
-        if (known <= (unsigned)tp) __builtin_amdgcn_s_sleep(1);
+      if (known <= (unsigned)tp) {
+        if (!spin_until<1, 1>(nullptr, nullptr, [&] { known = ld_ctl(&ctl[1]); return known > (unsigned)tp; })) {
+          __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          known = 0xFFFFFFFFu;   // (released: x is garbage, the error word says so)
+        }
       }
       const double x0 = kr < krows ? ld_sc1(y + k0 + kr) : 0.0;
       const double x1 = kr + 1 < krows ? ld_sc1(y + k0 + kr + 1) : 0.0;
@@ -2816,20 +2865,17 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
       // x_{B+1} is polled directly (y starts as the all-ones NaN pattern, which no fp64 arithmetic
       // produces -- b must not hold it either, trsv_lower_t's contract): no progress-word round trip
       // on the chain.  The spin is bounded: a producer that has not published after spin_limit
-      // sleeps raises the sticky device error word *err (bit 0), which the host reads with the
-      // Newton step's readback and turns into IPM_HIP_ERROR -- the step is never used silently.
+      // wall-clock bound (s_memrealtime, ipm_spin_ticks[1]) raises the sticky device error word *err (bit 0),
+      // which the host reads with the Newton step's readback and turns into IPM_HIP_ERROR -- the step
+      // is never used silently.
       if (tid < TB2) {
         double v = 0.0;
         if (tid < krows) {
-          for (unsigned spin = 0;; ++spin) {
-            v = ld_sc1(y + k0 + tid);
-            if (__double_as_longlong(v) != TRSV_PENDING) break;
-            if (spin >= spin_limit) {
-              __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
+          if (!spin_until<1, 1>(nullptr, nullptr, [&] {
+                v = ld_sc1(y + k0 + tid);
+                return __double_as_longlong(v) != TRSV_PENDING;
+              }))
+            __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         sm.sx[tid] = v;
       }
@@ -2884,9 +2930,10 @@ static void trsv_chain(hipStream_t st, bool fwd, int64_t n, const double* L, int
     hipLaunchKernelGGL(k_trsv_chain<false>, dim3(grid), dim3(256), 0, st, n, nblk, L, ldl, b, bstride, y, ctl);
 }
 
-static std::atomic<unsigned> g_trsv_spin_limit{1u << 20};
+// the chain poll's bound in microseconds of wall clock (a sleep count depends on the
+// clock and a descheduled producer); 0 restores the default 1 s
 static std::atomic<int> g_trsv_delay_ticket{-1};
-void set_trsv_spin_limit(unsigned lim) { g_trsv_spin_limit.store(lim ? lim : (1u << 20)); }
+void set_trsv_spin_limit(unsigned us) { set_spin_ticks(1, us); }
 void set_trsv_publish_delay(int ticket) { g_trsv_delay_ticket.store(ticket); }
 
 // L^T x = b (b read with stride bstride, e.g. the bordered row of a Cholesky factor); ctl: 2 words
@@ -2905,7 +2952,7 @@ void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const
   const int grid = std::min(nblk, 256);
   hipMemsetAsync(x, 0xFF, n * sizeof(double), st);   // TRSV_PENDING in every row
   hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl,
-                     err, g_trsv_spin_limit.load(std::memory_order_relaxed),
+                     err,
                      g_trsv_delay_ticket.load(std::memory_order_relaxed));
 }
 

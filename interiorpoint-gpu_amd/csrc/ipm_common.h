@@ -75,6 +75,11 @@ void syrk_lower(hipStream_t s, int64_t n, int64_t k, double alpha, const double*
 //   (the GEMM of the Cholesky panel / trailing update, general rectangle)
 void gemm_nt_sub(hipStream_t s, int64_t m, int64_t n, int64_t k, const double* A, int64_t lda,
                  const double* B, int64_t ldb, double* C, int64_t ldc);
+// C(i, j) = sum_k X[k][i] Y[k][j] over the FULL ni x nj rectangle (column-major C, ldc; X, Y
+// k-major): a product whose two triangles are computed separately, e.g. the non-symmetric
+// S = A (H^-1 A^T) of the infeasible-start block elimination
+void gemm_kk(hipStream_t s, int64_t ni, int64_t nj, int64_t k, const double* X, int64_t ldx, const double* Y,
+             int64_t ldy, double* C, int64_t ldc);
 
 // Cholesky (column-major lower, in place). info_dev: device int (0 or first failing column, 1-based)
 // ws: device workspace of potrf_ws_doubles(n) doubles: two panels' inverted diagonal blocks and
@@ -153,6 +158,12 @@ void trsv_lower_t(hipStream_t s, int64_t n, const double* L, int64_t ldl, const 
 // spin bound (sleeps) of the backward solve's chain poll; 0 restores the default 2^20 (debug knob:
 // ipm_debug_set_trsv_spin_limit)
 void set_trsv_spin_limit(unsigned lim);
+// bound (microseconds of wall clock, 0 = default 1 s) of every wait inside the ticketed Cholesky
+// (debug knob: ipm_debug_set_potrf_spin_limit); a missed bound makes *info = POTRF_INFO_SPIN (-1000)
+void set_potrf_spin_limit_us(unsigned us);
+constexpr int POTRF_INFO_SPIN = -1000;
+// debug knob: the k-th lstsq_sym_factor call from now reports non-convergence (-1: off)
+void set_lstsq_fail_call(int k);
 // debug knob: the workgroup holding this ticket of the backward solve sleeps ~7 ms before it
 // publishes its progress word (-1: none)
 void set_trsv_publish_delay(int ticket);
@@ -175,6 +186,8 @@ void getrs(hipStream_t s, int64_t n, int64_t nrhs, const double* LU, int64_t lda
 // factor = eigendecomposition (A full column-major -> eigenvectors in place, ws[0:n] the
 // pseudo-inverse weights), apply = B (row-major n x nrhs) <- H^+ B.  rb: lazily created library
 // handle slot.  ws: lstsq_ws_doubles(n, nrhs) doubles.  Return 0, or -1 on a library error.
+// *info_dev is STICKY: the factor sets it to 1 on non-convergence and never clears it (the caller
+// zeroes it once before a group of factorizations and reads it after all of them).
 int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs);
 int lstsq_sym_factor(void** rb, hipStream_t s, int64_t n, double* A, int64_t lda, double* ws, int* info_dev);
 int lstsq_sym_apply(void** rb, hipStream_t s, int64_t n, int64_t nrhs, const double* V, int64_t ldv, double* B,

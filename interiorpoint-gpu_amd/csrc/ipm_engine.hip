@@ -552,6 +552,11 @@ extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double
   int inf;
   std::memcpy(&inf, h->hbuf, sizeof(int));
   if (info) *info = inf;
+  if (inf < 0) {
+    h->err = "Cholesky: a wait inside the factorization ran past its wall-clock bound (info " + std::to_string(inf) +
+             "); the factor is not valid";
+    return IPM_HIP_ERROR;
+  }
   return inf == 0 ? IPM_OK : IPM_NOT_POSITIVE_DEFINITE;
 }
 
@@ -612,6 +617,7 @@ extern "C" int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, 
   if (n == 0 || nrhs == 0) return IPM_OK;
   double* lw = scratch(h, (size_t)lstsq_ws_doubles(n, nrhs) * sizeof(double));
   if (!lw) { h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  HIPCHK(h, hipMemsetAsync(h->dinfo, 0, sizeof(int), h->stream));   // (the factor's info is sticky)
   if (lstsq_sym_factor(&h->rb, h->stream, n, A, lda, lw, h->dinfo) ||
       lstsq_sym_apply(&h->rb, h->stream, n, nrhs, A, lda, B, ldb, lw)) {
     h->err = "least-squares library call failed";
@@ -701,6 +707,16 @@ extern "C" int ipm_problem_sizes(ipm_problem* pr, int64_t* out) {
 
 extern "C" int ipm_debug_set_trsv_spin_limit(unsigned limit) {
   set_trsv_spin_limit(limit);
+  return IPM_OK;
+}
+
+extern "C" int ipm_debug_set_potrf_spin_limit(unsigned microseconds) {
+  set_potrf_spin_limit_us(microseconds);
+  return IPM_OK;
+}
+
+extern "C" int ipm_debug_lstsq_fail_call(int k) {
+  set_lstsq_fail_call(k);
   return IPM_OK;
 }
 
@@ -978,6 +994,13 @@ int readback(ipm_problem* pr, Readback& r, bool want_info) {
     h->err = "least squares: the Jacobi eigensolver did not converge (numpy: SVD did not converge in Linear Least Squares)";
     return IPM_LINALG_NOT_CONVERGED;
   }
+  if (r.info < 0 || r.info2 < 0) {
+    // a Cholesky wait ran past its bound (POTRF_INFO_SPIN): the factor is garbage, not "not PD"
+    hipMemsetAsync(pr->info, 0, 2 * sizeof(int), st);
+    h->err = "Cholesky: a wait inside the factorization ran past its wall-clock bound (info " +
+             std::to_string(std::min(r.info, r.info2)) + "); the Newton step was discarded";
+    return IPM_HIP_ERROR;
+  }
   int derr;
   std::memcpy(&derr, hb + 4 * RB_INFO_TRSV_ERR, sizeof(int));
   if (derr) {
@@ -1210,9 +1233,12 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     }
     copy(st, pr->tmpn, pr->g, n);
     potrs_lower(st, n, 1, pr->H, pr->ldh, pr->tmpn, 1, pr->W2, pr->ctl, pr->xinv, trsv_err(pr));
-    // S = A Y (lower)
+    // S = A Y: the reference factors np.matmul(A, A11_inv_AT) with scipy's cho_factor, which reads
+    // the UPPER triangle (lower=False; NewtonSolverInfeasibleStart.py:473-477).  A Y is not exactly
+    // symmetric in rounding (Y carries the solve's errors), so the factored triangle is the one the
+    // reference reads: the lower triangle of (A Y)^T, i.e. X = Y, Y = A^T in the SYRK form
     SyrkEpi e;
-    syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
+    syrk_lower(st, p, n, 1.0, pr->Ybuf, p, d.AT, p, nullptr, 0.0, pr->Sbuf, lds, e);
     potrf_lower(st, p, pr->Sbuf, lds, pr->info + 1, pr->pws);
     // w = S^-1 (b2 - A hg)
     gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
@@ -1236,10 +1262,12 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   getrs(st, n, p, pr->H, pr->ldh, pr->piv, pr->Ybuf, p);
   copy(st, pr->tmpn, pr->g, n);
   getrs(st, n, 1, pr->H, pr->ldh, pr->piv, pr->tmpn, 1);
-  SyrkEpi e;
-  syrk_lower(st, p, n, 1.0, d.AT, p, pr->Ybuf, p, nullptr, 0.0, pr->Sbuf, lds, e);
-  rc = expand_full_inplace(pr, pr->Sbuf, p, lds);
-  if (rc) return rc;
+  // S = A Y in FULL, both triangles computed (np.matmul(A, A11_inv_AT), :527-529): the LU reads
+  // all of it, and at large t the asymmetry of A Y (the solve's rounding in Y) steers the step.
+  // A mirrored lower triangle instead moved lp_eq_ineq's x* by 2.9e-3 (oracle emulation, DESIGN
+  // §2.1), where the reference's own LU-rounding spread is 5e-8.  Column-major: S(i, j) at
+  // Sbuf[j * lds + i] = sum_k A^T[k][i] Y[k][j]
+  gemm_kk(st, p, p, n, d.AT, p, pr->Ybuf, p, pr->Sbuf, lds);
   getrf(st, p, pr->Sbuf, lds, pr->pivp, pr->info + 1, lw);
   gemv_n(st, p, n, 1.0, d.A, d.lda, pr->tmpn, 0.0, pr->r2);
   lincomb(st, p, 1.0, pr->Axb, -1.0, pr->r2, pr->wv);
@@ -1292,29 +1320,38 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
     if (e != hipSuccess) { h->err = hipGetErrorString(e); return IPM_HIP_ERROR; }
     return IPM_OK;
   };
+  // an eigensolve that did not converge (np.linalg.lstsq raising LinAlgError inside the reference's
+  // Newton loop) ends this Newton solve as a failure, as the reference's try/except does
+  // (NewtonSolver.py:148-155, NewtonSolverInfeasibleStart.py:161-164); other errors propagate
+  auto bail = [&](int rc) {
+    if (rc != IPM_LINALG_NOT_CONVERGED) return rc;
+    const int r2 = finish(it + 1, false, stat_valid, stat);
+    res->linalg_error = 1;
+    return r2;
+  };
 
   for (it = 0; it < o->max_iters; ++it) {
     gradient_at(pr, x, t);
     if (!pr->eq) {
       // ------------------------------------------------ feasible start (NewtonSolver.py)
       int rc = direction_feasible(pr, t, o);
-      if (rc) return rc;
+      if (rc) return bail(rc);
       prep_linesearch_dirs(pr);
       enqueue_scalars(pr, x, false, nullptr);
       int64_t k0 = 0;
       candidate_pass(pr, x, tab.alpha[0], o->beta);
       rc = readback(pr, rb, true);
-      if (rc) return rc;
+      if (rc) return bail(rc);
       if (rb.info != 0 && !pr->use_backup && !pr->diag) {
         // Cholesky failed: permanent LU fallback (Q9); H must be rebuilt (potrf overwrote it)
         pr->use_backup = true;
         rc = direction_feasible(pr, t, o);
-        if (rc) return rc;
+        if (rc) return bail(rc);
         prep_linesearch_dirs(pr);
         enqueue_scalars(pr, x, false, nullptr);
         candidate_pass(pr, x, tab.alpha[0], o->beta);
         rc = readback(pr, rb, false);
-        if (rc) return rc;
+        if (rc) return bail(rc);
       }
       const double fx = t * f_at(pr, rb.sc, 0.0) - rb.sc[SC_SUMLOG0];
       const double gc = rb.sc[SC_GX];
@@ -1420,7 +1457,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       const int lsm = o->linesearch_mode;
       if (lsm != IPM_LS_EXACT) {
         rc = table_step(&step);
-        if (rc) return rc;
+        if (rc) return bail(rc);
       }
       if (lsm == IPM_LS_EXACT || lsm == IPM_LS_COMPARE) {
         if (pr->socp) {
@@ -1430,7 +1467,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
         const Readback rb0 = rb;                     // g.x, g.dx, x[n], dx[n] of this step
         double se = 0.0;
         rc = exact_step(&se);
-        if (rc) return rc;
+        if (rc) return bail(rc);
         rb = rb0;
         if (lsm == IPM_LS_COMPARE) {
           ++res->ls_compared;
@@ -1454,7 +1491,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       // ------------------------------------------------ infeasible start
       bool lae = false;
       int rc = direction_infeasible(pr, x, v, t, o, &lae);
-      if (rc) return rc;
+      if (rc) return bail(rc);
       prep_linesearch_dirs(pr);
       // r = ||[g + A^T v ; A x - b]||  (pieces)
       const ipm_problem_desc& d = pr->d;
@@ -1466,7 +1503,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       int64_t k0 = 0;
       candidate_pass(pr, x, tab.alpha[0], o->beta);
       rc = readback(pr, rb, true);
-      if (rc) return rc;
+      if (rc) return bail(rc);
       // info[0]: H, info[1]: S (Cholesky paths)
       const int info2 = rb.info2;
       if (pr->diag) {
@@ -1477,7 +1514,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
       } else if ((rb.info != 0 || info2 != 0) && !pr->use_backup) {
         pr->use_backup = true;
         rc = direction_infeasible(pr, x, v, t, o, &lae);
-        if (rc) return rc;
+        if (rc) return bail(rc);
         prep_linesearch_dirs(pr);
         gemv_t(st, pr->p, pr->n, 1.0, d.A, d.lda, v, nullptr, 0.0, pr->ATv, pr->part, pr->part_elems);
         lincomb(st, pr->n, 1.0, pr->g, 1.0, pr->ATv, pr->tmpn);
@@ -1486,7 +1523,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
         enqueue_scalars(pr, x, true, v);
         candidate_pass(pr, x, tab.alpha[0], o->beta);
         rc = readback(pr, rb, false);
-        if (rc) return rc;
+        if (rc) return bail(rc);
       }
       const double r0 = std::sqrt(rb.sc[SC_R0A] + rb.sc[SC_R0B]);
       int64_t kd = -1, kstuck = -1;
@@ -1497,7 +1534,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
           k0 = k;
           candidate_pass(pr, x, tab.alpha[k0], o->beta);
           rc = readback(pr, rb, false);
-          if (rc) return rc;
+          if (rc) return bail(rc);
         }
         ++backtracks;
         if (rb.mask & (1ull << (k - k0))) { kd = k; break; }
@@ -1536,7 +1573,7 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
         };
         int64_t rk0 = kd;
         rc = resid_pass(rk0);
-        if (rc) return rc;
+        if (rc) return bail(rc);
         int64_t ks = kd;
         rn = std::sqrt(rb.sums[0]);
         int attempt = 0;
@@ -1551,11 +1588,11 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
             barrier_at(ks);
             rk0 = ks;
             rc = resid_pass(rk0);
-            if (rc) return rc;
+            if (rc) return bail(rc);
           } else if (ks >= rk0 + NCAND) {
             rk0 = ks;
             rc = resid_pass(rk0);
-            if (rc) return rc;
+            if (rc) return bail(rc);
           }
           rn = std::sqrt(rb.sums[ks - rk0]);
         }

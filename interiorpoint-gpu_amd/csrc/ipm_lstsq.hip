@@ -24,11 +24,14 @@
 // eigenvalues fall below gelsd's cut anyway.  Small systems (n <= JWG_MAX) run the whole iteration in
 // ONE workgroup (no launches per round); larger ones one rotation + one update launch per round and
 // a 4-byte readback per sweep.  Non-convergence within JMAX_SWEEPS sets *info_dev = 1 (the host
-// raises LinAlgError like numpy's "SVD did not converge").
+// raises LinAlgError like numpy's "SVD did not converge"); the word is sticky -- a factorization
+// never clears it, so of several eigensolves in one Newton step (the block elimination's H and S)
+// a failed one cannot be overwritten by a later converged one.
 // Right-hand sides use the engine's row-major convention: B is n x nrhs, element (i, j) at
 // B[i * ldb + j].
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <vector>
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
     if (srot == 0) break;
     __syncthreads();
   }
-  if (tid == 0) *info = sweep < JMAX_SWEEPS ? 0 : 1;
+  if (tid == 0 && sweep >= JMAX_SWEEPS) *info = 1;   // sticky: never cleared here
 }
 
 // large n: one round = rotations (k_jacobi_rot) + the two-sided update (k_jacobi_upd)
@@ -276,6 +279,10 @@ __global__ __launch_bounds__(256) void k_vt(int64_t n, int64_t nrhs, const doubl
 
 void lstsq_release(void* rb) { (void)rb; }
 
+static std::atomic<int> g_fail_call{-1};
+void set_lstsq_fail_call(int k) { g_fail_call.store(k); }
+__global__ void k_set_flag(int* p) { *p = 1; }
+
 // ws: f (n) | frob2 + counters (64) | V (n^2) | rotation pairs (n) + (c, s) (2n) | T (n * nrhs)
 int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs) {
   return n + 64 + n * n + 3 * (n + 2) + std::max<int64_t>(nrhs, 1) * n;
@@ -316,10 +323,11 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
         return -1;
       if (h == 0) break;
     }
-    const int inf = sweep < JMAX_SWEEPS ? 0 : 1;
-    hipMemcpyAsync(info_dev, &inf, sizeof(int), hipMemcpyHostToDevice, st);
-    hipStreamSynchronize(st);   // (inf lives on this host stack frame)
+    if (sweep >= JMAX_SWEEPS) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, st, info_dev);   // sticky
   }
+  // debug knob: this call reports non-convergence
+  if (g_fail_call.load() >= 0 && g_fail_call.fetch_sub(1) == 0)
+    hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, st, info_dev);
   hipLaunchKernelGGL(k_jacobi_finish, dim3(1), dim3(256), 0, st, n, A, lda, V, f);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -82,6 +82,44 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- bounded waits on other workgroups of the same launch (the ticketed Cholesky, its split
+// trailing tiles, the persistent backward solve).  A wait gives up after a bound on the
+// constant-rate GPU wall clock (s_memrealtime; 100 MHz on MI355X, the host converts microseconds
+// with hipDeviceAttributeWallClockRate) and records the failure: info (if still 0) becomes
+// POTRF_INFO_SPIN -- negative, never a LAPACK column -- and the launch's failure word is raised, so
+// every later launch of the factorization returns at once and every other waiter of this launch
+// stops waiting (it sees failw).  The host turns a negative info into IPM_HIP_ERROR: the factor is
+// never used.  The bounds live in a device global read only on the slow path (after 16 polls), so
+// the waits hold no extra registers in the kernels around them.  [0]: Cholesky, [1]: backward solve.
+static __device__ unsigned long long ipm_spin_ticks[2] = {100000000ull, 100000000ull};   // 1 s
+__device__ __forceinline__ void spin_fail(int* info, unsigned* failw) {
+  if (info) atomicCAS(info, 0, POTRF_INFO_SPIN);
+  __threadfence();
+  if (failw) atomicCAS(failw, 0u, 0xFFFFFFF0u);
+}
+// poll done() with s_sleep(SLEEP) in between; true once done, false when the bound ran out (the
+// failure is recorded in info / failw, either may be null) or the launch has already failed (failw)
+template <int SLEEP, int WHICH = 0, class Done>
+__device__ __forceinline__ bool spin_until(int* info, unsigned* failw, Done done) {
+  if (done()) return true;
+  unsigned long long t0 = 0;
+  for (unsigned it = 0;; ++it) {
+    __builtin_amdgcn_s_sleep(SLEEP);
+    if (done()) return true;
+    if ((it & 15u) != 0u) continue;
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (it == 0) {
+      t0 = now;
+      continue;
+    }
+    if (failw && __hip_atomic_load(failw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+    if (now - t0 > ipm_spin_ticks[WHICH]) {
+      spin_fail(info, failw);
+      return false;
+    }
+  }
+}
+
 // BM = 128 (4 x 4 MFMA tiles per wave) for large grids, 64 (2 x 2) when the 128-tile grid
 // would leave CUs idle.  WJ = waves along j (2: 256 threads, 2 workgroups per CU; 4: 512 threads).
 // PAD > 0 pads the LDS allocation so that only ONE workgroup fits a CU and no Cholesky panel
@@ -129,7 +167,7 @@ template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool 
           int LOOP = 0, int LAZYC = 0, bool CST = false>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
                                           double* part = nullptr, unsigned* pflag = nullptr, int64_t kb = -1,
-                                          int64_t ke = -1) {
+                                          int64_t ke = -1, int* sinfo = nullptr, unsigned* failw = nullptr) {
   using M = MfCfg<BM_, WJ>;
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
   IPM_TSTAMP(0);
@@ -435,7 +473,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   //      cdna_hip_programming.md §3) -> 16 consecutive lanes store 16 consecutive i
   if (SPLIT == 2) {
     if (tid == 0)
-      while (__hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) __builtin_amdgcn_s_sleep(2);
+      spin_until<2>(sinfo, failw, [&] { return __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u; });
     __syncthreads();
   }
   if (CST && cinit && SPLIT == 0) {

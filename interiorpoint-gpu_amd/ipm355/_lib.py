@@ -60,7 +60,7 @@ class NewtonOpts(C.Structure):
 class NewtonResult(C.Structure):
     _fields_ = [("iters", I32), ("success", I32), ("stat_valid", I32), ("use_backup", I32),
                 ("stat", F64), ("last_step", F64), ("backtracks", I64), ("ls_compared", I64),
-                ("ls_flips", I64)]
+                ("ls_flips", I64), ("linalg_error", I64)]
 
 
 EXPORTS = {
@@ -96,6 +96,8 @@ EXPORTS = {
     "ipm_set_timing": (C.c_int, [P, C.c_int]),
     "ipm_debug_set_trsv_spin_limit": (C.c_int, [C.c_uint]),
     "ipm_debug_set_trsv_publish_delay": (C.c_int, [C.c_int]),
+    "ipm_debug_set_potrf_spin_limit": (C.c_int, [C.c_uint]),
+    "ipm_debug_lstsq_fail_call": (C.c_int, [C.c_int]),
     # batched ADMM Lasso (ipm_lasso.hip; ipm355/lasso.py)
     "ipm_gemm_tn": (C.c_int, [P, I64, I64, I64, F64, P, I64, P, I64, F64, P, I64]),
     "ipm_transpose": (C.c_int, [P, I64, I64, P, I64, P, I64]),

@@ -78,7 +78,9 @@ class NewtonSolver:
             np.copyto(v0, v.cpu().numpy())
             v = v0
         stat = r.stat if r.stat_valid else None
-        if not self.suppress_print and r.iters >= self.max_iters and not r.success:
+        if not self.suppress_print and r.linalg_error:
+            print("OVERFLOW ERROR: Problem likely unbounded")      # (NewtonSolver.py:148-155)
+        elif not self.suppress_print and r.iters >= self.max_iters and not r.success:
             print("REACHED MAX ITERATIONS: Problem likely infeasible or unbounded")
         return xd, v, int(r.iters), stat, bool(r.success)
 

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r4a
+timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r4a/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR|passed|failed" gpurun_out/r4a/pytest.log | tail -15
+if [ $rc -gt 1 ]; then exit $rc; fi
+REPS=2 scripts/ab.sh gpurun_out/r4a/ab "--steps 20 --warmup 2" build/abl/r3k/libipm355.so interiorpoint-gpu_amd/ipm355/libipm355.so

@@ -15,7 +15,7 @@ import os
 import sys
 import types
 
-os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")   # (rerun_threads children set their own)
 sys.dont_write_bytecode = True
 REF = "/root/reference"
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -408,16 +408,109 @@ def lstsq_singular():
                                                             linear_solve_method=meth))
 
 
-def eq_ineq_methods():
+def _lu_unblocked(A):
+    """Right-looking unblocked LU with partial pivoting (LAPACK's pivot rule): the same algorithm
+    class as LAPACK's blocked recursive dgetrf, rounded differently -- the LU-rounding probe below."""
+    A = np.array(A, dtype=float, copy=True)
+    n = A.shape[0]
+    piv = np.arange(n)
+    for k in range(n):
+        p = k + int(np.argmax(np.abs(A[k:, k])))
+        if p != k:
+            A[[k, p]] = A[[p, k]]
+            piv[[k, p]] = piv[[p, k]]
+        if A[k, k] != 0:
+            A[k + 1:, k] /= A[k, k]
+            A[k + 1:, k + 1:] -= np.outer(A[k + 1:, k], A[k, k + 1:])
+    return A, piv
+
+
+def _solve_unblocked(A, B):
+    LU, piv = _lu_unblocked(A)
+    B = np.asarray(B, dtype=float)
+    vec = B.ndim == 1
+    X = (B[:, None] if vec else B)[piv].copy()
+    n = LU.shape[0]
+    for k in range(n):
+        X[k + 1:] -= np.outer(LU[k + 1:, k], X[k])
+    for k in range(n - 1, -1, -1):
+        X[k] /= LU[k, k]
+        X[:k] -= np.outer(LU[:k, k], X[k])
+    return X[:, 0] if vec else X
+
+
+def lu_rounding_envelope(name, cls, kwargs):
+    """The reference's sensitivity to the rounding of its LU (the device's LU is a
+    right-looking blocked one, LAPACK's dgetrf a recursive one): the same solve with np.linalg.solve
+    / np.linalg.inv replaced, at run time, by an unblocked right-looking LU of the same pivoting
+    rule, and once more at another OpenBLAS thread count (a child process; small n usually runs one
+    thread either way).  The spread joins the fixture's sens_* envelope (sens_key gets "+lu")."""
+    import subprocess
+    path = os.path.join(HERE, name + ".npz")
+    z = dict(np.load(path, allow_pickle=False))
+    base_x, base_v = z["xstar"], float(z["value"])
+    kw = {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in kwargs.items()}
+    kw.setdefault("check_cvxpy", False)
+    kw.setdefault("suppress_print", True)
+    orig = np.linalg.solve, np.linalg.inv
+    np.linalg.solve = _solve_unblocked
+    np.linalg.inv = lambda A: _solve_unblocked(A, np.eye(np.asarray(A).shape[0]))
+    try:
+        s = cls(**kw)
+        v = s.solve()
+    finally:
+        np.linalg.solve, np.linalg.inv = orig
+    wx = float(np.linalg.norm(np.asarray(s.xstar) - base_x) / np.linalg.norm(base_x))
+    wv = float(abs(v - base_v) / max(abs(base_v), 1e-300))
+    stable = list(s.inner_iters) == list(z["inner_iters"])
+    out = {"lu_unblocked": (wx, wv, list(s.inner_iters))}
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="4", OMP_NUM_THREADS="4", PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "rerun_threads", name], env=env,
+                       capture_output=True, text=True, timeout=3600)
+    if r.returncode == 0:
+        xs, vt, it = np.load(os.path.join(HERE, f".{name}_threads.npz"), allow_pickle=False).values()
+        os.remove(os.path.join(HERE, f".{name}_threads.npz"))
+        wt = float(np.linalg.norm(xs - base_x) / np.linalg.norm(base_x))
+        out["threads4"] = (wt, float(abs(float(vt) - base_v) / max(abs(base_v), 1e-300)), list(it))
+        wx, wv = max(wx, out["threads4"][0]), max(wv, out["threads4"][1])
+        stable &= list(it) == list(z["inner_iters"])
+    z["sens_lu_xstar_rel"] = np.array(out["lu_unblocked"][0])
+    z["sens_lu_iters"] = np.array(out["lu_unblocked"][2])
+    z["sens_xstar_rel"] = np.array(max(float(z["sens_xstar_rel"]), wx))
+    z["sens_value_rel"] = np.array(max(float(z["sens_value_rel"]), wv))
+    z["sens_iters_stable"] = np.array(bool(z["sens_iters_stable"]) and stable)
+    z["sens_key"] = np.array(str(z["sens_key"]) + "+lu")
+    np.savez_compressed(path, **z)
+    print(f"{name}: LU-rounding envelope {out}; sens x* {float(z['sens_xstar_rel']):.1e}, "
+          f"iters stable {bool(z['sens_iters_stable'])}")
+
+
+def _eq_ineq_kwargs():
+    rng = np.random.default_rng(6)
+    n = 80
+    Aeq = rng.uniform(-2, 2, (20, n)); C = rng.uniform(-2, 2, (10, n)); xf = rng.uniform(-2, 2, n)
+    return dict(c=rng.uniform(-2, 2, n), A=Aeq, b=Aeq @ xf, C=C, d=C @ xf + 1, lower_bound=-3, upper_bound=3,
+                **problems.LP_KWARGS)
+
+
+def eq_ineq_methods(methods=("np_lstsq", "np_solve", "direct")):
     """lp_eq_ineq (dense infeasible start + phase 1) under np_solve / direct / np_lstsq: the steps
-    near t ~ 1e7 have a nearly singular H, so the reference's own spread decides the bar."""
-    for meth in ("np_lstsq",):
-        rng = np.random.default_rng(6)
-        n = 80
-        Aeq = rng.uniform(-2, 2, (20, n)); C = rng.uniform(-2, 2, (10, n)); xf = rng.uniform(-2, 2, n)
-        run_solve(f"meth_lp_eq_ineq_{meth}", RefLP, dict(c=rng.uniform(-2, 2, n), A=Aeq, b=Aeq @ xf, C=C,
-                                                         d=C @ xf + 1, lower_bound=-3, upper_bound=3,
-                                                         **problems.LP_KWARGS, linear_solve_method=meth))
+    near t ~ 1e7 have a nearly singular H, so the reference's own spread decides the bar -- for the
+    LU methods including its sensitivity to the LU's rounding (lu_rounding_envelope)."""
+    for meth in methods:
+        kw = dict(_eq_ineq_kwargs(), linear_solve_method=meth)
+        run_solve(f"meth_lp_eq_ineq_{meth}", RefLP, kw)
+        if meth != "np_lstsq":
+            lu_rounding_envelope(f"meth_lp_eq_ineq_{meth}", RefLP, kw)
+
+
+def _rerun_threads(name):
+    """child of lu_rounding_envelope: the same solve at this process's OpenBLAS thread count"""
+    meth = name.rsplit("meth_lp_eq_ineq_", 1)[1]
+    s = RefLP(check_cvxpy=False, suppress_print=True, **dict(_eq_ineq_kwargs(), linear_solve_method=meth))
+    v = s.solve()
+    np.savez(os.path.join(HERE, f".{name}_threads.npz"), x=np.asarray(s.xstar), v=np.array(v),
+             it=np.array(s.inner_iters))
 
 
 if __name__ == "__main__":
@@ -430,6 +523,10 @@ if __name__ == "__main__":
         npy_lp()
     elif sys.argv[1:] == ["eq_ineq_methods"]:
         eq_ineq_methods()
+    elif sys.argv[1:] == ["eq_ineq_lu"]:
+        eq_ineq_methods(("np_solve", "direct"))
+    elif sys.argv[1:2] == ["rerun_threads"]:
+        _rerun_threads(sys.argv[2])
     elif sys.argv[1:] == ["lstsq_singular"]:
         lstsq_singular()
     elif sys.argv[1:] == ["eq_box_stable"]:

@@ -25,9 +25,9 @@ METHOD_CASES = {f"meth_{case}_{meth}": kind
 # rank-deficient H (LP, n > m, no bounds): np_lstsq, and the Cholesky class on its lstsq backup
 # (make_golden.py lstsq_singular) -- minimum-norm steps, where an LU solve has no answer
 METHOD_CASES.update({f"lsq_sing_lp{n}_{meth}": "LP" for n in (100, 64) for meth in ("np_lstsq", "cholesky")})
-# dense infeasible start + phase 1 with np_lstsq (make_golden.py eq_ineq_methods; the reference's
-# np_solve / direct runs of this case end stuck at the precision floor)
-METHOD_CASES["meth_lp_eq_ineq_np_lstsq"] = "LP"
+# dense infeasible start + phase 1 with np_lstsq / np_solve / direct (make_golden.py eq_ineq_methods;
+# the LU fixtures' envelope includes the reference's sensitivity to its LU's rounding, round 4)
+METHOD_CASES.update({f"meth_lp_eq_ineq_{meth}": "LP" for meth in ("np_lstsq", "np_solve", "direct")})
 
 # kwargs that are stored as scalars in the fixture but are not array inputs
 _SCALAR_KW = {"t0", "mu", "epsilon", "alpha", "beta", "max_inner_iters", "max_outer_iters",

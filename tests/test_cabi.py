@@ -47,7 +47,7 @@ def test_struct_sizes_match_header_layout():
     from ipm355 import _lib
     # ipm_problem_desc: 4 int32 + 8-byte fields ... computed by ctypes with C alignment
     assert ctypes.sizeof(_lib.NewtonOpts) == 4 * 4 + 4 * 8 + 8 + 8
-    assert ctypes.sizeof(_lib.NewtonResult) == 4 * 4 + 5 * 8
+    assert ctypes.sizeof(_lib.NewtonResult) == 4 * 4 + 6 * 8
     assert ctypes.sizeof(_lib.ProblemDesc) % 8 == 0
 
 

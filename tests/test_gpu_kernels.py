@@ -321,3 +321,36 @@ def test_trsv_backward_solve_late_publisher(ticket):
     finally:
         h.lib.ipm_debug_set_trsv_publish_delay(-1)
     np.testing.assert_array_equal(x0, x1)
+
+
+def test_potrf_wait_bound_fails_loudly():
+    """every wait inside the ticketed Cholesky (k_potrf_block) has a wall-clock bound.
+    Shrunk to 1 us (debug knob) the waits run out: ipm_potrf must report IPM_HIP_ERROR with
+    info = -1000 (never a LAPACK column, never a silently wrong factor), the failure must drain
+    every later launch (the call returns), and with the default bound the same matrix factors
+    correctly again (nothing sticky left in the workspace)."""
+    from ipm355 import _lib as L
+    h = handle()
+    n = 4096
+    rng = np.random.default_rng(17)
+    M = rng.normal(size=(n + 8, n)) * 2.0 ** -4
+    A = M.T @ M + n * np.eye(n)
+    tripped = 0
+    try:
+        h.lib.ipm_debug_set_potrf_spin_limit(1)
+        for _ in range(3):
+            rc, info = potrf(dev(A), n, n)
+            if rc == L.IPM_HIP_ERROR:
+                assert info == -1000, info
+                tripped += 1
+            else:
+                assert rc == 0 and info == 0, (rc, info)
+    finally:
+        h.lib.ipm_debug_set_potrf_spin_limit(0)
+    assert tripped >= 1
+    Hm = dev(A)
+    rc, info = potrf(Hm, n, n)
+    assert rc == 0 and info == 0
+    got = np.tril(host(Hm).T)
+    ref = np.linalg.cholesky(A)
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-10 * np.abs(ref).max())
