@@ -15,7 +15,7 @@ SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_en
 # eigensolver included, ipm_lstsq.hip)
 LIBS     :=
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
-HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
+HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_diag2.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
 
 all: $(OUT)
 

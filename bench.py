@@ -29,7 +29,6 @@ bounded sample of the same workload at 1 and all available BLAS threads.
 from __future__ import annotations
 
 import argparse
-import contextlib
 import hashlib
 import json
 import math
@@ -285,10 +284,11 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
     if args.concurrent:
-        # each instance = its stream + its Cholesky panel stream; HIP maps streams onto
-        # GPU_MAX_HW_QUEUES hardware queues (4 by default) -- streams sharing a queue serialise.
-        # Must be set before the HIP runtime starts (the box presets 4: override it, <= 32 allowed).
-        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("IPM_HW_QUEUES", "16")
+        # each instance = its own stream; HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
+        # (4 by default) -- streams sharing a queue serialise.  Must be set before the HIP runtime
+        # starts (the box presets 4: override it, <= 32 allowed).
+        from ipm355 import dist as _D
+        _D.configure_queues(int(os.environ.get("IPM_HW_QUEUES", "16")))
 
     import torch
     import torch.distributed as dist
@@ -317,23 +317,28 @@ def main():
 
     kwargs = dict({"qp": problems.QP_KWARGS, "lp": problems.LP_KWARGS, "socp": problems.SOCP_KWARGS}[args.problem])
     Cls = {"qp": ipm355.QPSolver, "lp": ipm355.LPSolver, "socp": ipm355.SOCPSolver}[args.problem]
-    if args.instances == 1:
-        seeds = [rank]                         # headline: one n=8192 instance per GPU, seed = rank
-    else:                                      # config 4: instances r::world of world*I, seeds 1000 + index
-        seeds = [1000 + i for i in D.shard(args.instances * world, rank, world)]
-    insts = [make_instance(args.n, args.m, seed=sd, dev=dev, problem=args.problem) for sd in seeds]
+    # instances of this rank: ipm355.dist's round-robin shard (the API a user calls for config 4);
+    # headline: instance index = rank (one n=8192 instance per GPU, seed = rank); config 4
+    # (--instances I): indices r::world of world*I, seeds 1000 + index
+    n_inst = world * args.instances
+    indices = D.shard(n_inst, rank, world)
+    seeds = {i: (i if args.instances == 1 else 1000 + i) for i in indices}
+    insts = {i: make_instance(args.n, args.m, seed=seeds[i], dev=dev, problem=args.problem) for i in indices}
 
-    def new_solver(k, feasible):
-        inst, xf = insts[k]
-        kw = dict(inst, **kwargs)
-        if feasible:
-            kw["x0"] = xf.copy()               # strictly feasible -> phase 1 skipped (Q11)
-        return Cls(check_cvxpy=False, suppress_print=True, device=dev_index, **kw)
+    def builder(feasible):
+        def make(i):
+            inst, xf = insts[i]
+            kw = dict(inst, **kwargs)
+            if feasible:
+                kw["x0"] = xf.copy()           # strictly feasible -> phase 1 skipped (Q11)
+            return kw
+        return make
 
-    streams = [torch.cuda.Stream(device=dev) for _ in insts] if args.concurrent else [None] * len(insts)
-
-    def on(stream):
-        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+    def new_shard(feasible):
+        # ipm355.dist.Shard: solvers built (inputs resident in HBM) on this rank's GPU; with
+        # --concurrent each instance has its own HIP stream and is solved from its own host thread
+        return D.Shard(builder(feasible or args.problem == "socp"), indices, Cls, None, device=dev_index,
+                       concurrent=args.concurrent)
 
     if args.problem == "socp":
         args.phase = "barrier"               # M5 starts strictly feasible (phase 1 skipped, Q11)
@@ -342,58 +347,43 @@ def main():
     w1 = (args.warmup + 1) // 2
     for feasible, budget in ((False, w1), (True, args.warmup - w1)):   # warmup, untimed
         if budget > 0:
-            for k in range(len(insts) if args.concurrent else 1):
-                with on(streams[k]):
-                    new_solver(k, feasible or args.problem == "socp").solve(iteration_budget=budget)
-    with on(streams[0]):
-        h = L.Handle.get(dev_index)
+            new_shard(feasible).solve(iteration_budget=budget)
     import ctypes
     res, evidence, hbm_rates = {}, {}, {}
     for name, budget in segs:
         if budget <= 0:
             res[name] = dict(iters=0, seconds=0.0, kkt_ms=0.0, potrf_ms=0.0, kkt_flops=0.0, N=0)
             continue
-        solvers = []
-        for k, stm in enumerate(streams):           # inputs resident in HBM before timing
-            with on(stm):
-                solvers.append(new_solver(k, name == "barrier"))
-        fm0 = solvers[0].phase1_solver.phase1_fm if name == "phase1" else solvers[0].fm
+        sh = new_shard(name == "barrier")   # inputs resident in HBM before timing
+        s0 = sh.solvers[0]
+        fm0 = s0.phase1_solver.phase1_fm if name == "phase1" else s0.fm
         kkt_flops = fm0.prob.kkt_flops()[0]
+        h = fm0.prob.handle                # (instance 0's handle: the timings below are its own)
         h.lib.ipm_set_timing(h.ptr, 1)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        if args.concurrent:
-            from concurrent.futures import ThreadPoolExecutor
-
-            def run(k):
-                with on(streams[k]):
-                    solvers[k].solve(iteration_budget=budget)
-            with ThreadPoolExecutor(max_workers=len(solvers)) as ex:
-                list(ex.map(run, range(len(solvers))))
-        else:
-            for s in solvers:
-                s.solve(iteration_budget=budget)
+        local = sh.solve(iteration_budget=budget)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
         a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         h.lib.ipm_last_timings(h.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
-        iters = 0
-        for s in solvers:
-            p1 = s.phase1_solver
-            iters += sum(s.inner_iters) + (sum(p1.inner_iters) if p1 is not None and name == "phase1" else 0)
-        res[name] = dict(iters=float(iters), seconds=el, kkt_ms=a.value, potrf_ms=b.value, kkt_flops=kkt_flops,
+        h.lib.ipm_set_timing(h.ptr, 0)
+        # Newton iterations of this segment (phase-1 ones only in the phase-1 segment: the barrier
+        # segment starts strictly feasible)
+        iters = float(sum(v[1] for v in local.values()))
+        res[name] = dict(iters=iters, seconds=el, kkt_ms=a.value, potrf_ms=b.value, kkt_flops=kkt_flops,
                          N=args.n + (1 if name == "phase1" else 0))
         if rank == 0:
             # after the timed region: rank 0's own evidence (trace/iterate vs the reference fixture,
             # HBM-kernel GB/s on this solver's buffers)
-            evidence[name] = fixture_parity(solvers[0], name, seeds[0], args, budget)
+            evidence[name] = fixture_parity(s0, name, seeds[indices[0]], args, budget)
             if args.problem in ("qp", "lp"):
                 hbm_rates[name] = hbm_kernels(fm0.prob)
-        del solvers
+        del sh, s0, fm0
 
     keys = ("iters", "seconds", "kkt_ms", "potrf_ms")
     row = [res[nm][k] for nm, _ in segs for k in keys]
@@ -489,7 +479,7 @@ def main():
                                          f"bounds, test_SOCP kwargs; {args.steps} barrier-phase iterations from the "
                                          f"strictly feasible x0 (phase 1 skipped)")
         if not args.no_cpu and world == 1 and args.problem == "qp":
-            rec["cpu_baseline"] = cpu_baseline(insts[0][0], kwargs, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(insts[indices[0]][0], kwargs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -88,37 +88,111 @@ def gather_results(local: dict, n_instances: int, device=None, xs: dict | None =
     return (out, X) if xs is not None else out
 
 
+class Shard:
+    """This rank's instances, built on this rank's GPU and ready to solve (inputs resident in HBM).
+
+    concurrent=True (config 4): every instance gets its own HIP stream -- its solver and native
+    handle are created under ``torch.cuda.stream(stream)`` -- and ``solve()`` runs the instances
+    from one host thread each (the native calls release the GIL), so their kernels overlap on the
+    GPU.  The HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default;
+    streams sharing a queue serialise): call ``configure_queues()`` before anything initialises
+    the GPU.  concurrent=False: one after another on the current stream."""
+
+    def __init__(self, make_instance, indices, solver_cls, kwargs=None, device=None, concurrent=False):
+        import torch
+        self.indices = list(indices)
+        self.dev = local_device(device)
+        self.concurrent = bool(concurrent)
+        self.streams = ([torch.cuda.Stream(device=torch.device("cuda", self.dev)) for _ in self.indices]
+                        if self.concurrent else [None] * len(self.indices))
+        self.solvers = []
+        for i, st in zip(self.indices, self.streams):
+            with _on(st):
+                s = solver_cls(check_cvxpy=False, suppress_print=True, device=self.dev, **make_instance(i),
+                               **(kwargs or {}))
+            if s.dev.index != self.dev:
+                raise RuntimeError(f"solver placed on {s.dev}, rank owns cuda:{self.dev}")
+            self.solvers.append(s)
+
+    def solve(self, **solve_kwargs):
+        """Solve every instance (solve_kwargs go to each solver's solve(), e.g. iteration_budget);
+        returns {index: (value, Newton iterations incl. phase 1, seconds)}."""
+        import torch
+
+        def one(k):
+            s = self.solvers[k]
+            t0 = time.perf_counter()
+            with _on(self.streams[k]):
+                value = s.solve(**solve_kwargs)
+                if self.streams[k] is not None:
+                    self.streams[k].synchronize()
+            p1 = getattr(s, "phase1_solver", None)
+            iters = int(sum(s.inner_iters)) + (int(sum(p1.inner_iters)) if p1 is not None else 0)
+            return self.indices[k], (value, iters, time.perf_counter() - t0)
+        if self.concurrent and len(self.solvers) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=len(self.solvers)) as ex:
+                out = dict(ex.map(one, range(len(self.solvers))))
+        else:
+            out = dict(one(k) for k in range(len(self.solvers)))
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(self.dev)
+        return out
+
+    def xstar(self):
+        return {i: s.xstar for i, s in zip(self.indices, self.solvers)}
+
+
+def _on(stream):
+    import contextlib
+
+    import torch
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
+def configure_queues(queues: int = 16) -> bool:
+    """Give the HIP runtime `queues` hardware queues per process (GPU_MAX_HW_QUEUES, read once when
+    the runtime starts) so that concurrent instances do not serialise on shared queues.  Returns
+    False when it is too late (the runtime already started); the box presets 4, gpurun allows 32."""
+    import torch
+    if torch.cuda.is_initialized():
+        return False
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(queues))
+    return True
+
+
+def build_shard(make_instance, n_instances: int, solver_cls, kwargs=None, device=None, concurrent=False) -> Shard:
+    """This rank's instances r::world of n_instances, built (not solved) on this rank's GPU."""
+    rank, world = _world()
+    return Shard(make_instance, shard(n_instances, rank, world), solver_cls, kwargs, device, concurrent)
+
+
 def solve_sharded(make_instance, n_instances: int, solver_cls=None, kwargs=None, device=None,
-                  solve_fn=None, gather_x: bool = False):
+                  solve_fn=None, gather_x: bool = False, concurrent: bool = False, solve_kwargs=None):
     """Solve this rank's shard on this rank's GPU, then gather every instance's (value, iters, seconds).
 
     make_instance(i) -> dict of constructor arguments for instance i (seeded by i);
     solver_cls: ipm355.LPSolver / QPSolver / SOCPSolver; kwargs: shared solver kwargs.
     device: this rank's GPU (default LOCAL_RANK); every solver is built on it.
+    concurrent: solve this rank's instances concurrently, one HIP stream + host thread each (Shard).
+    solve_kwargs: passed to every solve() (e.g. iteration_budget).
     solve_fn(i) -> (value, iters[, x*]) overrides the solver (host-logic tests run it without a GPU).
     gather_x: also gather every instance's x* -> returns (table, X).
     """
     rank, world = _world()
-    dev = local_device(device)
     local, xs = {}, {}
-    for i in shard(n_instances, rank, world):
-        t0 = time.perf_counter()
-        if solve_fn is not None:
+    if solve_fn is not None:
+        for i in shard(n_instances, rank, world):
+            t0 = time.perf_counter()
             r = solve_fn(i)
-            value, iters = r[0], r[1]
-            x = r[2] if len(r) > 2 else None
-        else:
-            s = solver_cls(check_cvxpy=False, suppress_print=True, device=dev, **make_instance(i),
-                           **(kwargs or {}))
-            if s.dev.index != dev:
-                raise RuntimeError(f"solver placed on {s.dev}, rank owns cuda:{dev}")
-            value = s.solve()
-            p1 = getattr(s, "phase1_solver", None)
-            iters = int(sum(s.inner_iters)) + (int(sum(p1.inner_iters)) if p1 is not None else 0)
-            x = s.xstar
-        local[i] = (value, iters, time.perf_counter() - t0)
+            local[i] = (r[0], r[1], time.perf_counter() - t0)
+            if gather_x:
+                xs[i] = r[2] if len(r) > 2 else None
+    else:
+        sh = build_shard(make_instance, n_instances, solver_cls, kwargs, device, concurrent)
+        local = sh.solve(**(solve_kwargs or {}))
         if gather_x:
-            xs[i] = x
+            xs = sh.xstar()
     if gather_x:
         nx = len(next(iter(xs.values()))) if xs else 0
         if world > 1 and dist_initialized():

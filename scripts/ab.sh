@@ -15,6 +15,6 @@ for rep in $(seq 1 ${REPS:-2}); do
     env $envs IPM355_LIB=$PWD/$lib timeout -k 10 ${T:-300} python bench.py --no-cpu $args > "$out/run.json" 2> "$out/run.err"
     rc=$?
     if [ $rc -ne 0 ]; then echo "$spec: bench rc=$rc"; tail -5 "$out/run.err"; exit $rc; fi
-    python3 -c "import json;d=json.load(open('$out/run.json'));print('$spec', round(d['value'],2), 'potrf', round(d['potrf']['avg_ms'],3), 'syrk', round(d['kkt_syrk']['avg_launch_ms'],3))"
+    python3 -c "import json;d=json.load(open('$out/run.json'));p=d.get('parity') or {};print('$spec', round(d['value'],2), 'potrf', round(d['potrf']['avg_ms'],3), 'syrk', round(d['kkt_syrk']['avg_launch_ms'],3), 'steps_identical', [v.get('steps_identical') for v in p.values() if v])"
   done
 done

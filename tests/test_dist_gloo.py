@@ -104,3 +104,24 @@ def test_solve_sharded_places_solvers_on_the_rank_device(monkeypatch):
     _FakeSolver.seen = []
     D.solve_sharded(lambda i: {}, 1, _FakeSolver, device=5)
     assert _FakeSolver.seen == [5]
+
+
+def test_shard_solves_every_instance_once_with_solve_kwargs(monkeypatch):
+    """ipm355.dist.Shard (the config-4 product path): built once (inputs resident), solve() passes
+    its keyword arguments (e.g. iteration_budget) to every instance and reports value, Newton
+    iterations (phase 1 included) and seconds per instance index."""
+    calls = []
+
+    class _Budgeted(_FakeSolver):
+        def solve(self, **kw):
+            calls.append(kw)
+            return 2.5
+
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    sh = D.build_shard(lambda i: {}, 3, _Budgeted)
+    assert sh.indices == [0, 1, 2] and not sh.concurrent
+    out = sh.solve(iteration_budget=7)
+    assert sorted(out) == [0, 1, 2] and all(v[0] == 2.5 and v[1] == 3 for v in out.values())
+    assert calls == [{"iteration_budget": 7}] * 3
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")     # (restored after the test)
+    assert D.configure_queues(16) in (True, False)

@@ -354,3 +354,46 @@ def test_potrf_wait_bound_fails_loudly():
     got = np.tril(host(Hm).T)
     ref = np.linalg.cholesky(A)
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-10 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("n,ncols", [(130, 129), (200, 200), (1030, 1030), (2049, 2048), (4097, 4096), (8193, 8192)])
+def test_potrf_diag_role2(n, ncols, monkeypatch):
+    """The round-4 diagonal role (ipm_diag2.h: one sweep solves the whole 16-column block column and
+    L_JJ^-1; two barriers per step), forced with IPM_DIAG2=1 on full and partial last panels and on
+    the bordered Newton layout (ncols = n - 1): the factor against NumPy's, the rows below it
+    against L21 = A21 L11^-T."""
+    monkeypatch.setenv("IPM_DIAG2", "1")
+    rng = np.random.default_rng(n + 3 * ncols)
+    M = rng.normal(size=(n + 5, n))
+    A = M.T @ M + n * np.eye(n)
+    Hm = dev(A.T.copy())
+    rc, info = potrf(Hm, n, n, ncols=ncols)
+    assert rc == 0 and info == 0
+    got = host(Hm).T
+    L11 = np.linalg.cholesky(A[:ncols, :ncols])
+    np.testing.assert_allclose(np.tril(got[:ncols, :ncols]), L11, rtol=1e-10, atol=1e-10 * np.abs(L11).max())
+    if ncols < n:
+        L21 = np.linalg.solve(L11, A[ncols:, :ncols].T).T
+        np.testing.assert_allclose(got[ncols:, :ncols], L21, rtol=1e-10, atol=1e-10 * np.abs(L21).max())
+
+
+@pytest.mark.parametrize("diag2", ["0", "1"])
+def test_potrf_not_pd_info_matches_lapack(diag2, monkeypatch):
+    """A non-positive pivot inside a diagonal role: LAPACK's info (first failing column, 1-based)
+    with either role, and the factorization ends (every later launch sees the failure word)."""
+    import scipy.linalg
+    monkeypatch.setenv("IPM_DIAG2", diag2)
+    n = 1030
+    rng = np.random.default_rng(21)
+    M = rng.normal(size=(n + 5, n))
+    A = M.T @ M + n * np.eye(n)
+    k = 300                      # make the leading (k+1) x (k+1) minor indefinite
+    A[k, k] = -abs(A[k, k])
+    rc, info = potrf(dev(A.T.copy()), n, n)
+    try:
+        scipy.linalg.cholesky(A, lower=True)
+        ref = 0
+    except np.linalg.LinAlgError as e:
+        ref = int(str(e).split("-th")[0].split()[-1])
+    assert info == ref == k + 1, (info, ref)
+    assert rc != 0

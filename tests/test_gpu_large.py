@@ -196,17 +196,21 @@ def test_linesearch_flip_rate(name, monkeypatch):
         assert same
 
 
-def test_m4_shard_on_one_gpu():
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_m4_shard_on_one_gpu(concurrent):
     """Config 4 shard: eight of the 64 M4 instances (seeds 1000..1007, n=2048, m=512) solved by the
     sharded driver (ipm355.dist.solve_sharded, world 1 -> every instance on this GPU), x* gathered
-    through the same table the multi-GPU run all_gathers, each against its reference fixture."""
+    through the same table the multi-GPU run all_gathers, each against its reference fixture.
+    concurrent=True: the product path of config 4's per-GPU concurrency -- one HIP
+    stream + host thread per instance (ipm355.dist.Shard) -- with the same bars, identical iteration
+    counts included."""
     from ipm355 import dist
     from ipm355 import QPSolver
     names = [f"m4_qp_{sd}" for sd in range(1000, 1008)]
     zs = [_fixture(nm) for nm in names]
     insts = [_instance(z)[1] for z in zs]
     tab, X = dist.solve_sharded(lambda i: {k: v for k, v in insts[i].items()}, len(insts), QPSolver,
-                                device=0, gather_x=True)
+                                device=0, gather_x=True, concurrent=concurrent)
     for i, z in enumerate(zs):
         err = rel(X[i], z["xstar"])
         ref_iters = int(sum(z["inner_iters"]) + sum(z["phase1_inner_iters"]))
