@@ -1,4 +1,4 @@
-# Build the MI355X (gfx950) shared library and the oracle's C pieces.
+# Build the MI355X (gfx950) shared library libipm355.so (the oracle is pure Python: nothing to build).
 #   make            -> interiorpoint-gpu_amd/ipm355/libipm355.so
 #   make clean
 HIPCC    ?= /opt/rocm/bin/hipcc
@@ -15,7 +15,7 @@ SRCS     := $(SRC_DIR)/ipm_blas.hip $(SRC_DIR)/ipm_barrier.hip $(SRC_DIR)/ipm_en
 # eigensolver included, ipm_lstsq.hip)
 LIBS     :=
 OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
-HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_diag2.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
+HDRS     := $(SRC_DIR)/ipm_common.h $(SRC_DIR)/ipm_mfma.h $(SRC_DIR)/ipm_barrier.h $(SRC_DIR)/ipm_handle.h include/ipm355.h
 
 all: $(OUT)
 

@@ -939,7 +939,6 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 }
 #undef STAMP
 
-#include "ipm_diag2.h"
 
 // control words of one Cholesky launch (k_potrf_block; the header of block_ctl_words)
 enum {
@@ -1224,7 +1223,6 @@ struct BlockArgs {
   int64_t sa = 0, sb = 0;
   int rpad_a = 0, rpad_b = 0;
   int rowprio = 0;              // s_setprio of the non-critical row chunks (IPM_ROWPRIO)
-  int diag2 = 0;                // full panels' diagonal role: diag_role2 (ipm_diag2.h) with IPM_DIAG2=1
 };
 #ifndef FLEX_PROG
 #define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
@@ -1258,7 +1256,6 @@ __device__ __forceinline__ unsigned cu_key() {
 
 union BlockSmem {
   DiagSmem d;
-  Diag2Smem d2;
   MfSmem<128, 2> g128;
   MfSmem<64, 2> g64;
   MfSmem<32, 2> g32;
@@ -1490,10 +1487,9 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     ROLE(pb ? 3 : 1);
     if (pb) wait_words(&b.ctl[CTL_NF], 1, (unsigned)b.nnf, b.info, failw);
     else wait_la(0, b.wa - 1);
-    if (b.diag2)
-      diag_role2<true>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d2, &b.ctl[CTL_FAIL]);
-    else
-      diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
+    // (the round-4 one-sweep role, tools/diag2_lab.hip + ipm_diag2.h, ran 5 % faster alone but not
+    // inside the launch, and instantiating it here raised the kernel's SGPR spills 80 -> 700+)
+    diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
     return;
   }
   if (kind == K_ROW) {
@@ -2134,7 +2130,10 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       Plan p;
       {
         std::lock_guard<std::mutex> lk(mu);
-        auto& v = cache[{n, ncols, (split_on ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0) | (lazy_on ? 4 : 0)}];
+        // (split_here in the key: with IPM_ROWPOS=1 a launch that may not split must never reuse a
+        // plan with q > 0 -- its split scratch and flags are not set up)
+        auto& v = cache[{n, ncols, (split_here ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0) | (lazy_on ? 4 : 0) |
+                                       (lazy2_on ? 8 : 0) | (vec ? 16 : 0)}];
         if ((int64_t)v.size() < nblocks) v.assign(nblocks, Plan{});
         if (v[bk].q < 0) {
           Plan& w = v[bk];
@@ -2154,6 +2153,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         }
         p = v[bk];
       }
+      if (!split_here) p.q = 0;
       b.s_full -= p.q;
       b.ns = b.nstrip + b.s_full + 2 * p.q;
       b.sa = std::min(p.sa, b.ns);
@@ -2168,10 +2168,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     }
     static const int rowprio = [] { const char* e = getenv("IPM_ROWPRIO"); return e ? atoi(e) : 0; }();
     b.rowprio = rowprio;
-    {
-      const char* e = getenv("IPM_DIAG2");   // (read per call: tests compare both roles)
-      b.diag2 = (e && e[0] == '1') ? 1 : 0;
-    }
     if (defer) {
       // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
       b.gX = ds->X;

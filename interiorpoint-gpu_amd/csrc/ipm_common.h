@@ -183,15 +183,18 @@ inline int64_t getrf_ws_doubles(int64_t n) { return 64 * (n + 1); }
 void getrs(hipStream_t s, int64_t n, int64_t nrhs, const double* LU, int64_t lda, const int64_t* piv,
            double* B, int64_t ldb);
 // minimum-norm least squares on a symmetric matrix, np.linalg.lstsq(H, B, rcond=None) (ipm_lstsq.hip):
-// factor = eigendecomposition (A full column-major -> eigenvectors in place, ws[0:n] the
-// pseudo-inverse weights), apply = B (row-major n x nrhs) <- H^+ B.  rb: lazily created library
+// factor = eigendecomposition (A full column-major; ws <- the eigenvectors V and the pseudo-inverse
+// weights, A <- V^T), apply = B (row-major n x nrhs) <- H^+ B (W = the factored A).  The blocked
+// Jacobi above n = 256 does one 4-byte readback per sweep.  rb: lazily created library
 // handle slot.  ws: lstsq_ws_doubles(n, nrhs) doubles.  Return 0, or -1 on a library error.
 // *info_dev is STICKY: the factor sets it to 1 on non-convergence and never clears it (the caller
 // zeroes it once before a group of factorizations and reads it after all of them).
 int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs);
 int lstsq_sym_factor(void** rb, hipStream_t s, int64_t n, double* A, int64_t lda, double* ws, int* info_dev);
-int lstsq_sym_apply(void** rb, hipStream_t s, int64_t n, int64_t nrhs, const double* V, int64_t ldv, double* B,
+int lstsq_sym_apply(void** rb, hipStream_t s, int64_t n, int64_t nrhs, const double* W, int64_t ldw, double* B,
                     int64_t ldb, double* ws);
+// column-major lower triangle -> full symmetric, in place (the upper triangle is overwritten)
+void sym_expand_inplace(hipStream_t s, int64_t n, double* M, int64_t ld);
 void lstsq_release(void* rb);
 
 // small helpers

@@ -1,4 +1,7 @@
-// The diagonal role of the ticketed Cholesky, round 4 (included by ipm_blas.hip after diag_role).
+// A diagonal role for the ticketed Cholesky, round 4 -- LAB ONLY (tools/diag2_lab.hip includes it
+// after ipm_blas.hip).  Measured: 63.7 K vs 67.3 K cycles for the round-3 role alone, no change
+// inside k_potrf_block, and its instantiation there raised the SGPR spills 80 -> 700+, so the
+// library does not include it.
 //
 // One workgroup (4 waves) factors the 128 x 128 diagonal block of a panel held in LDS as 36 packed
 // 16 x 16 blocks, one 16-column block column J = 0..7 at a time (NewtonSolver.py:303-313's

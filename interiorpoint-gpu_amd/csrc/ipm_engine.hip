@@ -93,6 +93,7 @@ struct ipm_problem {
   int* kend_d = nullptr;
   double* Gd = nullptr;
   double* sws = nullptr;   // KKT SYRK split tail (syrk_split_ws_doubles)
+  double* lsw = nullptr;   // least-squares workspace (lstsq_ws_doubles; null when the method never uses it)
   DeferSyrk dsy;
   bool defer_on = false;
 };
@@ -228,6 +229,15 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->part_elems = pe;
   pr->part = c.take<double>(pe);
   if (!pr->diag && (pr->m > 0 || pr->socp)) pr->sws = c.take<double>(syrk_split_ws_doubles(n));
+  // least squares (np_lstsq, and the Cholesky-failure backup Q9 of the feasible-start path): the
+  // eigensolver's V (n^2) and scratch live in the problem workspace, never grown on the hot path
+  {
+    int64_t lw = 0;
+    if (!pr->lu && !pr->diag && !pr->eq) lw = lstsq_ws_doubles(N, 1);
+    if (pr->lsq && pr->eq && !pr->diag) lw = lstsq_ws_doubles(n, p) + lstsq_ws_doubles(p, 1) + p * (p + (p & 1));
+    if (pr->lsq && pr->diag && pr->eq) lw = lstsq_ws_doubles(p, 1);
+    pr->lsw = lw > 0 ? c.take<double>(lw) : nullptr;
+  }
   pr->rowcone_d = c.take<int64_t>(pr->R + 1);
   pr->dslot_d = c.take<int64_t>(pr->K + 1);
   if (!pr->defer_d.empty()) {
@@ -1063,12 +1073,9 @@ int enqueue_scalars(ipm_problem* pr, const double* x, bool infeasible, const dou
 
 }  // namespace
 
-// symmetric expansion in place through a scratch of n*ld doubles (handle scratch; fallback path only)
+// symmetric expansion in place (the lower triangle mirrored into the upper; no scratch)
 static int expand_full_inplace(ipm_problem* pr, double* M, int64_t n, int64_t ld) {
-  double* tmp = scratch(pr->h, (size_t)std::max<int64_t>(n * ld, 1) * sizeof(double));
-  if (!tmp) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
-  sym_lower_to_full(S(pr), n, M, ld, tmp, ld);
-  copy(S(pr), M, tmp, n * ld);
+  sym_expand_inplace(S(pr), n, M, ld);
   return IPM_OK;
 }
 
@@ -1102,8 +1109,8 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     lincomb(st, pr->N, -1.0, pr->g, 0.0, nullptr, pr->dx);
     int rc = expand_full_inplace(pr, pr->H, pr->N, pr->ldh);
     if (rc) return rc;
-    double* lw = scratch(pr->h, (size_t)lstsq_ws_doubles(pr->N, 1) * sizeof(double));
-    if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+    double* lw = pr->lsw;
+    if (!lw) { pr->h->err = "no least-squares workspace"; return IPM_HIP_ERROR; }
     if (lstsq_sym_factor(&pr->h->rb, st, pr->N, pr->H, pr->ldh, lw, lsq_info(pr)) ||
         lstsq_sym_apply(&pr->h->rb, st, pr->N, 1, pr->H, pr->ldh, pr->dx, 1, lw)) {
       pr->h->err = "least-squares library call failed";
@@ -1133,10 +1140,10 @@ int direction_infeasible_lstsq(ipm_problem* pr, const double* v) {
   const int64_t n = pr->n, p = pr->p, lds = p + (p & 1);
   int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
   if (rc) return rc;
-  // one scratch carve (the handle scratch is shared: expand_full_inplace would reuse its start)
+  // the problem's least-squares workspace: H's factor, S's factor, a p x p temporary
   const int64_t wh = lstsq_ws_doubles(n, p), ws = lstsq_ws_doubles(p, 1);
-  double* lw = scratch(pr->h, (size_t)(wh + ws + std::max<int64_t>(p * lds, 1)) * sizeof(double));
-  if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+  double* lw = pr->lsw;
+  if (!lw) { pr->h->err = "no least-squares workspace"; return IPM_HIP_ERROR; }
   double* lws = lw + wh;
   double* stmp = lws + ws;
   void** rb = &pr->h->rb;
@@ -1188,8 +1195,8 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
       // NewtonSolverNPLstSqDiagonalInfeasibleStart (NewtonSolverInfeasibleStart.py:692-724): w = lstsq(S, r)
       int rc = expand_full_inplace(pr, pr->Sbuf, p, lds);
       if (rc) return rc;
-      lw = scratch(pr->h, (size_t)lstsq_ws_doubles(p, 1) * sizeof(double));
-      if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
+      lw = pr->lsw;
+      if (!lw) { pr->h->err = "no least-squares workspace"; return IPM_HIP_ERROR; }
       if (lstsq_sym_factor(&pr->h->rb, st, p, pr->Sbuf, lds, lw, lsq_info(pr))) {
         pr->h->err = "least-squares library call failed";
         return IPM_HIP_ERROR;
@@ -1255,7 +1262,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   // LU fallback: four np.linalg.solve (NewtonSolverInfeasibleStart.py:513-538)
   int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
   if (rc) return rc;
-  double* lw = scratch(pr->h, (size_t)std::max(getrf_ws_doubles(n), n * pr->ldh) * sizeof(double));
+  double* lw = scratch(pr->h, (size_t)getrf_ws_doubles(n) * sizeof(double));
   if (!lw) { pr->h->err = "scratch alloc failed"; return IPM_HIP_ERROR; }
   getrf(st, n, pr->H, pr->ldh, pr->piv, pr->info, lw);
   copy(st, pr->Ybuf, d.AT, n * p);

@@ -188,49 +188,212 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
   if (tid == 0 && sweep >= JMAX_SWEEPS) *info = 1;   // sticky: never cleared here
 }
 
-// large n: one round = rotations (k_jacobi_rot) + the two-sided update (k_jacobi_upd)
-__global__ void k_jacobi_rot(int n, int r, const double* __restrict__ A, int64_t lda, const double* frob2,
-                             int* __restrict__ part, double* __restrict__ cs, int* __restrict__ nrot) {
-  const int nn = n + (n & 1), half = nn / 2;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= half) return;
-  const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
-  int a, b;
-  circle_pair(nn, r, i, a, b);
-  const int p = min(a, b), q = max(a, b);
-  double c = 1.0, s = 0.0;
-  if (q < n && jacobi_rot(A[(int64_t)p * lda + p], A[(int64_t)q * lda + q], A[(int64_t)q * lda + p], tiny, c, s))
-    atomicAdd(nrot, 1);
-  part[i] = jpack(p, q, n);
-  cs[2 * i] = c;
-  cs[2 * i + 1] = s;
+// ---------------------------------------------------------------------------------------------
+// Large n: BLOCKED two-sided Jacobi.  The index range is cut into nb = ceil(n / 32) blocks of 32
+// (an odd count gets one empty block); every round pairs the blocks by the same circle ordering
+// and, for each pair (P, Q), diagonalises the 64 x 64 subproblem S = A[P u Q, P u Q] completely
+// (k_bj_eig: the cyclic Jacobi above, in LDS, one workgroup per pair) into S' = G^T S G.  The
+// orthogonal G (64 x 64) is then applied to the whole matrix on MFMA tiles -- rows
+// A[P u Q, :] <- G^T A[P u Q, :] (k_bj_rows), then columns A[:, P u Q] <- A[:, P u Q] G and
+// V[:, P u Q] <- V[:, P u Q] G (k_bj_cols) -- and the pair's own 64 x 64 block is replaced by the
+// diagonalised S' (whose rotated entries are exact zeros, like the 2 x 2 form's).  A sweep is
+// nb - 1 rounds; the sweeps stop when no subproblem rotated anything (the same per-entry tests as
+// the 2 x 2 method, so the stopping rule and the answer are the same).  Work per sweep ~12 n^3
+// flops on MFMA instead of n - 1 rounds of scattered 2 x 2 updates over all of A and V; a pair
+// whose subproblem did not rotate (most of them in the last sweeps) skips its updates.
+constexpr int BJ = 32;         // block size
+constexpr int BS = 2 * BJ;     // subproblem size
+constexpr int BLD = BS + 1;    // LDS leading dimension (odd: conflict-free row and column walks)
+
+__device__ __forceinline__ int64_t bj_index(int P, int Q, int k) {
+  return k < BJ ? (int64_t)P * BJ + k : (int64_t)Q * BJ + (k - BJ);
 }
 
-__global__ void k_jacobi_upd(int n, double* A, int64_t lda, double* V, const int* __restrict__ part,
-                             const double* __restrict__ cs) {
-  const int nn = n + (n & 1), half = nn / 2;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nA = (int64_t)half * half;
-  if (e < nA) {
-    const int P = (int)(e % half), Q = (int)(e / half);   // consecutive threads: consecutive row pairs
-    const int pp = part[P], pq = part[Q];
-    const double c1 = cs[2 * P], s1 = cs[2 * P + 1], c2 = cs[2 * Q], s2 = cs[2 * Q + 1];
-    if (c1 == 1.0 && s1 == 0.0 && c2 == 1.0 && s2 == 0.0) return;
-    jacobi_block(A, lda, pp, c1, s1, pq, c2, s2, P == Q);
-  } else if (e < nA + (int64_t)half * n) {
-    const int64_t f = e - nA;
-    const int P = (int)(f / n);
-    const int64_t k = f % n;
-    const int pp = part[P];
-    if (cs[2 * P] == 1.0 && cs[2 * P + 1] == 0.0) return;   // (singles always: identity)
-    jacobi_vcols(V, n, pp & 0xFFFF, pp >> 16, cs[2 * P], cs[2 * P + 1], k);
+// per-pair scratch: G (BS x BS, column-major) | S' (BS x BS) ; rot flags (one int per pair)
+__global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const double* __restrict__ A, int64_t lda,
+                                                const double* frob2, double* __restrict__ gbuf,
+                                                int* __restrict__ rflag, int* __restrict__ nrot,
+                                                int* __restrict__ info) {
+  __shared__ double S[BS * BLD], G[BS * BLD];
+  __shared__ double sc[BS / 2], ss[BS / 2];
+  __shared__ int sp[BS / 2], sq[BS / 2];
+  __shared__ int srot;
+  const int pair = blockIdx.x, tid = threadIdx.x;
+  int a, b;
+  circle_pair(nbp, r, pair, a, b);
+  const int P = min(a, b), Q = max(a, b);
+  // S from the lower triangle of A (symmetrised: the updates keep A symmetric only to rounding)
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, j = e / BS;
+    const int64_t gi = bj_index(P, Q, i), gj = bj_index(P, Q, j);
+    double v = 0.0;
+    if (gi < n && gj < n) v = gi >= gj ? A[gj * lda + gi] : A[gi * lda + gj];
+    S[j * BLD + i] = v;
+    G[j * BLD + i] = (i == j) ? 1.0 : 0.0;
+  }
+  const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
+  int total = 0, sweep = 0;
+  __syncthreads();
+  for (; sweep < JMAX_SWEEPS; ++sweep) {
+    if (tid == 0) srot = 0;
+    __syncthreads();
+    for (int rr = 0; rr < BS - 1; ++rr) {
+      if (tid < BS / 2) {
+        int x, y;
+        circle_pair(BS, rr, tid, x, y);
+        const int p = min(x, y), q = max(x, y);
+        double c = 1.0, s = 0.0;
+        if (jacobi_rot(S[p * BLD + p], S[q * BLD + q], S[q * BLD + p], tiny, c, s)) atomicAdd(&srot, 1);
+        sp[tid] = p;
+        sq[tid] = q;
+        sc[tid] = c;
+        ss[tid] = s;
+      }
+      __syncthreads();
+      // S <- J^T S J, 2 x 2 blocks (row pair I, column pair K)
+      for (int e = tid; e < (BS / 2) * (BS / 2); e += 256) {
+        const int I = e % (BS / 2), K = e / (BS / 2);
+        const double c1 = sc[I], s1 = ss[I], c2 = sc[K], s2 = ss[K];
+        if (s1 == 0.0 && s2 == 0.0) continue;   // (s == 0 <=> identity: jacobi_rot's c is then 1)
+        const int p1 = sp[I], q1 = sq[I], p2 = sp[K], q2 = sq[K];
+        const double x11 = S[p2 * BLD + p1], x12 = S[q2 * BLD + p1], x21 = S[p2 * BLD + q1], x22 = S[q2 * BLD + q1];
+        const double y11 = c1 * x11 - s1 * x21, y12 = c1 * x12 - s1 * x22;
+        const double y21 = s1 * x11 + c1 * x21, y22 = s1 * x12 + c1 * x22;
+        double z11 = c2 * y11 - s2 * y12, z12 = s2 * y11 + c2 * y12;
+        double z21 = c2 * y21 - s2 * y22, z22 = s2 * y21 + c2 * y22;
+        if (I == K) z12 = z21 = 0.0;
+        S[p2 * BLD + p1] = z11;
+        S[q2 * BLD + p1] = z12;
+        S[p2 * BLD + q1] = z21;
+        S[q2 * BLD + q1] = z22;
+      }
+      // G <- G J (columns p, q of every row k)
+      for (int e = tid; e < (BS / 2) * BS; e += 256) {
+        const int I = e / BS, k = e % BS;
+        const double c = sc[I], s = ss[I];
+        if (s == 0.0) continue;
+        const int p = sp[I], q = sq[I];
+        const double u = G[p * BLD + k], w = G[q * BLD + k];
+        G[p * BLD + k] = c * u - s * w;
+        G[q * BLD + k] = s * u + c * w;
+      }
+      __syncthreads();
+    }
+    const int nr = srot;
+    total += nr;
+    __syncthreads();
+    if (nr == 0) break;
+  }
+  double* go = gbuf + (int64_t)pair * 2 * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, j = e / BS;
+    go[e] = G[j * BLD + i];
+    go[BS * BS + e] = S[j * BLD + i];
+  }
+  if (tid == 0) {
+    rflag[pair] = total > 0 ? 1 : 0;
+    if (total > 0) atomicAdd(nrot, total);
+    if (sweep >= JMAX_SWEEPS) *info = 1;   // sticky: never cleared here
+  }
+}
+
+// One 64 x 64 output tile on fp64 MFMA (16x16x4; cdna_hip_programming.md §3 maps: A lane l:
+// A[l&15][l>>4], B lane l: B[l>>4][l&15], D lane l, reg r: D[(l>>4)+4r][l&15]).  Wave w computes
+// output rows [16 w, 16 w + 16) x all 64 columns; D(i, j) = sum_k opA(i, k) opB(k, j) with
+// opA(i, k) = LA[ia(i, k)] and opB(k, j) = LB[ib(k, j)] read from LDS; D goes back to LDS tile Out
+// (column-major, BLD) -- the caller stores it coalesced.
+template <class FA, class FB>
+__device__ __forceinline__ void bj_tile(FA fa, FB fb, double* Out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i0 = 16 * wv, li = lane & 15, lk = lane >> 4;
+  dbl4 acc[4];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) acc[jt] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < BS; k0 += 4) {
+    const double av = fa(i0 + li, k0 + lk);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, fb(k0 + lk, 16 * jt + li), acc[jt], 0, 0, 0);
+  }
+  __syncthreads();   // every operand read before Out (which may alias an operand) is written
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Out[(16 * jt + li) * BLD + i0 + lk + 4 * rr] = acc[jt][rr];
+  __syncthreads();
+}
+
+// rows: A[P u Q, c0 : c0 + 64] <- G^T A[P u Q, c0 : c0 + 64]
+__global__ __launch_bounds__(256) void k_bj_rows(int n, int nbp, int r, double* __restrict__ A, int64_t lda,
+                                                 const double* __restrict__ gbuf, const int* __restrict__ rflag) {
+  const int pair = blockIdx.y;
+  if (!rflag[pair]) return;
+  __shared__ double Gl[BS * BLD], X[BS * BLD];
+  int a, b;
+  circle_pair(nbp, r, pair, a, b);
+  const int P = min(a, b), Q = max(a, b), tid = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * BS;
+  const double* g = gbuf + (int64_t)pair * 2 * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int k = e % BS, j = e / BS;
+    Gl[j * BLD + k] = g[e];
+    const int64_t gi = bj_index(P, Q, k), gj = c0 + j;
+    X[j * BLD + k] = (gi < n && gj < n) ? A[gj * lda + gi] : 0.0;   // X(k, j)
+  }
+  __syncthreads();
+  // D(i, j) = sum_k G(k, i) X(k, j)
+  bj_tile([&](int i, int k) { return Gl[i * BLD + k]; }, [&](int k, int j) { return X[j * BLD + k]; }, X);
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, j = e / BS;
+    const int64_t gi = bj_index(P, Q, i), gj = c0 + j;
+    if (gi < n && gj < n) A[gj * lda + gi] = X[j * BLD + i];
+  }
+}
+
+// columns: M[r0 : r0 + 64, P u Q] <- M[r0 : r0 + 64, P u Q] G for M = A (z = 0) and V (z = 1);
+// in A the pair's own rows take the diagonalised S' instead
+__global__ __launch_bounds__(256) void k_bj_cols(int n, int nbp, int r, double* __restrict__ A, int64_t lda,
+                                                 double* __restrict__ V, int64_t ldv,
+                                                 const double* __restrict__ gbuf, const int* __restrict__ rflag) {
+  const int pair = blockIdx.y;
+  if (!rflag[pair]) return;
+  __shared__ double Gl[BS * BLD], Y[BS * BLD];
+  int a, b;
+  circle_pair(nbp, r, pair, a, b);
+  const int P = min(a, b), Q = max(a, b), tid = threadIdx.x;
+  const bool isA = blockIdx.z == 0;
+  double* M = isA ? A : V;
+  const int64_t ld = isA ? lda : ldv;
+  const int64_t r0 = (int64_t)blockIdx.x * BS;
+  const double* g = gbuf + (int64_t)pair * 2 * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, k = e / BS;
+    Gl[k * BLD + i] = g[e];   // G(i, k)
+    const int64_t gi = r0 + i, gk = bj_index(P, Q, k);
+    Y[k * BLD + i] = (gi < n && gk < n) ? M[gk * ld + gi] : 0.0;   // Y(i, k)
+  }
+  __syncthreads();
+  // D(i, j) = sum_k Y(i, k) G(k, j)
+  bj_tile([&](int i, int k) { return Y[k * BLD + i]; }, [&](int k, int j) { return Gl[j * BLD + k]; }, Y);
+  const double* sfin = g + BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, j = e / BS;
+    const int64_t gi = r0 + i, gj = bj_index(P, Q, j);
+    if (gi >= n || gj >= n) continue;
+    double v = Y[j * BLD + i];
+    if (isA) {
+      const int64_t blk = gi / BJ;
+      if (blk == P) v = sfin[j * BS + (int)(gi % BJ)];
+      else if (blk == Q) v = sfin[j * BS + BJ + (int)(gi % BJ)];
+    }
+    M[gj * ld + gi] = v;
   }
 }
 
 // eigenvalues (diagonal of the rotated A) -> pseudo-inverse weights f_i = 1/lambda_i if
-// |lambda_i| > eps * n * max|lambda| else 0 (gelsd's rcond=None rule); V -> A (eigenvectors in place)
-__global__ __launch_bounds__(256) void k_jacobi_finish(int64_t n, double* A, int64_t lda, const double* __restrict__ V,
-                                                       double* __restrict__ f) {
+// |lambda_i| > eps * n * max|lambda| else 0 (gelsd's rcond=None rule)
+__global__ __launch_bounds__(256) void k_jacobi_weights(int64_t n, const double* __restrict__ A, int64_t lda,
+                                                        double* __restrict__ f) {
   __shared__ double red[256];
   double m = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += 256) m = fmax(m, fabs(A[i * lda + i]));
@@ -245,8 +408,6 @@ __global__ __launch_bounds__(256) void k_jacobi_finish(int64_t n, double* A, int
     const double l = A[i * lda + i];
     f[i] = (fabs(l) > cut) ? 1.0 / l : 0.0;
   }
-  __syncthreads();   // every diagonal read before V overwrites A
-  for (int64_t e = threadIdx.x; e < n * n; e += 256) A[(e / n) * lda + (e % n)] = V[e];
 }
 
 // T(i, r) = f_i sum_k V(k, i) B(k, r): one wave per (i, r), lanes split k (V column i contiguous)
@@ -277,19 +438,44 @@ __global__ __launch_bounds__(256) void k_vt(int64_t n, int64_t nrhs, const doubl
   B[i * ldb + r] = acc;
 }
 
+// T (row-major n x nrhs) rows scaled by f
+__global__ void k_scale_rows(int64_t n, int64_t nrhs, const double* __restrict__ f, double* __restrict__ T) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < n * nrhs) T[e] *= f[e / nrhs];
+}
+
+// upper triangle <- lower triangle, in place (column-major, ld): the two element sets are
+// disjoint, so no scratch copy is needed
+__global__ void k_sym_expand(int64_t n, double* __restrict__ M, int64_t ld) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * n) return;
+  const int64_t i = e % n, j = e / n;
+  if (i < j) M[j * ld + i] = M[i * ld + j];
+}
+void sym_expand_inplace(hipStream_t st, int64_t n, double* M, int64_t ld) {
+  if (n > 1) hipLaunchKernelGGL(k_sym_expand, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, st, n, M, ld);
+}
+
 void lstsq_release(void* rb) { (void)rb; }
 
 static std::atomic<int> g_fail_call{-1};
 void set_lstsq_fail_call(int k) { g_fail_call.store(k); }
 __global__ void k_set_flag(int* p) { *p = 1; }
 
-// ws: f (n) | frob2 + counters (64) | V (n^2) | rotation pairs (n) + (c, s) (2n) | T (n * nrhs)
-int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs) {
-  return n + 64 + n * n + 3 * (n + 2) + std::max<int64_t>(nrhs, 1) * n;
+static inline int64_t bj_pairs(int64_t n) {
+  const int64_t nb = (n + BJ - 1) / BJ;
+  return (nb + (nb & 1)) / 2;
 }
+// ws: f (n) | frob2 + counters (64) | V (n^2, column-major, ld n) | per-pair G + S' | rot flags | T (n * nrhs)
+static inline int64_t ws_off_pairs(int64_t n) { return n + 64 + n * n; }
+static inline int64_t ws_off_t(int64_t n) {
+  return ws_off_pairs(n) + (n > JWG_MAX ? bj_pairs(n) * (2 * BS * BS + 1) : 0);
+}
+int64_t lstsq_ws_doubles(int64_t n, int64_t nrhs) { return ws_off_t(n) + std::max<int64_t>(nrhs, 1) * n; }
 
-// A (full symmetric, column-major, lda) -> eigenvectors V in place; ws[0:n] -> pseudo-inverse
-// weights f.  *info_dev = 0, or 1 when Jacobi did not converge within JMAX_SWEEPS sweeps.
+// A (full symmetric, column-major, lda): ws <- V (eigenvectors, column-major) and the
+// pseudo-inverse weights f; A <- W = V^T (column-major, lda), the operand layout of the MFMA apply.
+// *info_dev: set to 1 when Jacobi did not converge within JMAX_SWEEPS sweeps (sticky).
 // Returns 0, or -1 on a launch error.
 int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t lda, double* ws, int* info_dev) {
   (void)rb;
@@ -299,23 +485,24 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
   double* frob2 = ws + n;
   int* nrot = reinterpret_cast<int*>(ws + n + 8);
   double* V = ws + n + 64;
-  int* part = reinterpret_cast<int*>(V + n * n);
-  double* cs = V + n * n + (n + 2);
   hipLaunchKernelGGL(k_frob2, dim3(1), dim3(256), 0, st, n, A, lda, frob2);
   hipLaunchKernelGGL(k_eye, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, st, n, V);
   if (n <= JWG_MAX) {
     hipLaunchKernelGGL(k_jacobi_wg, dim3(1), dim3(1024), 0, st, (int)n, A, lda, V, frob2, info_dev);
   } else {
-    const int nn = (int)(n + (n & 1)), half = nn / 2;
-    const int64_t upd = (int64_t)half * half + (int64_t)half * n;
+    const int64_t nb = (n + BJ - 1) / BJ, nbp = nb + (nb & 1), np = nbp / 2, tiles = (n + BS - 1) / BS;
+    double* gbuf = ws + ws_off_pairs(n);
+    int* rflag = reinterpret_cast<int*>(gbuf + np * 2 * BS * BS);
     int sweep = 0;
     for (; sweep < JMAX_SWEEPS; ++sweep) {
       hipMemsetAsync(nrot, 0, sizeof(int), st);
-      for (int r = 0; r < nn - 1; ++r) {
-        hipLaunchKernelGGL(k_jacobi_rot, dim3((half + 255) / 256), dim3(256), 0, st, (int)n, r, A, lda, frob2, part,
-                           cs, nrot);
-        hipLaunchKernelGGL(k_jacobi_upd, dim3((unsigned)((upd + 255) / 256)), dim3(256), 0, st, (int)n, A, lda, V,
-                           part, cs);
+      for (int r = 0; r < (int)nbp - 1; ++r) {
+        hipLaunchKernelGGL(k_bj_eig, dim3((unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A, lda, frob2, gbuf,
+                           rflag, nrot, info_dev);
+        hipLaunchKernelGGL(k_bj_rows, dim3((unsigned)tiles, (unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A,
+                           lda, gbuf, rflag);
+        hipLaunchKernelGGL(k_bj_cols, dim3((unsigned)tiles, (unsigned)np, 2), dim3(256), 0, st, (int)n, (int)nbp, r,
+                           A, lda, V, n, gbuf, rflag);
       }
       int h = 0;
       if (hipMemcpyAsync(&h, nrot, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -328,20 +515,33 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
   // debug knob: this call reports non-convergence
   if (g_fail_call.load() >= 0 && g_fail_call.fetch_sub(1) == 0)
     hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, st, info_dev);
-  hipLaunchKernelGGL(k_jacobi_finish, dim3(1), dim3(256), 0, st, n, A, lda, V, f);
+  hipLaunchKernelGGL(k_jacobi_weights, dim3(1), dim3(256), 0, st, n, A, lda, f);
+  // W = V^T into A's storage (V column-major = row-major V^T)
+  transpose(st, n, n, V, n, A, lda);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// B (row-major n x nrhs, ldb) <- V diag(f) V^T B, with V, f from lstsq_sym_factor (same ws).
-int lstsq_sym_apply(void** rb, hipStream_t st, int64_t n, int64_t nrhs, const double* V, int64_t ldv, double* B,
+// B (row-major n x nrhs, ldb) <- V diag(f) V^T B, with V, f (ws) and W = V^T (A) from
+// lstsq_sym_factor.  Few right-hand sides: one pass over V per product (wave dot products);
+// many: two MFMA GEMMs (gemm_kk: C(i, j) = sum_k X[k][i] Y[k][j]).
+int lstsq_sym_apply(void** rb, hipStream_t st, int64_t n, int64_t nrhs, const double* W, int64_t ldw, double* B,
                     int64_t ldb, double* ws) {
   (void)rb;
   if (n <= 0 || nrhs <= 0) return 0;
   const double* f = ws;
-  double* T = ws + n + 64 + n * n + 3 * (n + 2);
-  const int64_t waves = n * nrhs;
-  hipLaunchKernelGGL(k_vtb, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, n, nrhs, V, ldv, B, ldb, f, T);
-  hipLaunchKernelGGL(k_vt, dim3((unsigned)((n * nrhs + 255) / 256)), dim3(256), 0, st, n, nrhs, V, ldv, T, B, ldb);
+  const double* V = ws + n + 64;
+  double* T = ws + ws_off_t(n);
+  if (nrhs < 8) {
+    const int64_t waves = n * nrhs;
+    hipLaunchKernelGGL(k_vtb, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, n, nrhs, V, n, B, ldb, f, T);
+    hipLaunchKernelGGL(k_vt, dim3((unsigned)((n * nrhs + 255) / 256)), dim3(256), 0, st, n, nrhs, V, n, T, B, ldb);
+  } else {
+    // T (row-major n x nrhs): T(i, r) = sum_k V(k, i) B(k, r) -> C(r, i) with X = B, Y = W (W[k][i] = V(k, i))
+    gemm_kk(st, nrhs, n, n, B, ldb, W, ldw, T, nrhs);
+    hipLaunchKernelGGL(k_scale_rows, dim3((unsigned)((n * nrhs + 255) / 256)), dim3(256), 0, st, n, nrhs, f, T);
+    // B(i, r) = sum_k V(i, k) T(k, r) -> C(r, i) with X = T, Y = V (V[k][i] = V(i, k), column-major)
+    gemm_kk(st, nrhs, n, n, T, nrhs, V, n, B, ldb);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

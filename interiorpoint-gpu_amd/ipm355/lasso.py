@@ -96,11 +96,13 @@ class LassoSolver:
             raise NameError("name 'cp' is not defined")   # LassoSolver.py:147 (cp.linalg.eigvalsh)
         n = self.n
         # Qinv and its transpose: the transpose is the k-major operand of every product with Qinv
-        self.Qinv = torch.empty((n, n), dtype=torch.float64, device=self.dev)
+        # (Qinv itself is scratch of the solve: only the transpose is kept)
+        Qinv = torch.empty((n, n), dtype=torch.float64, device=self.dev)
         self.QinvT = torch.empty((n, n), dtype=torch.float64, device=self.dev)
         info = C.c_int(0)
-        rc = lib.ipm_lasso_qinv(h.ptr, self.m, n, L.dptr(Ad), n, float(rho), L.dptr(self.Qinv), L.dptr(self.QinvT),
+        rc = lib.ipm_lasso_qinv(h.ptr, self.m, n, L.dptr(Ad), n, float(rho), L.dptr(Qinv), L.dptr(self.QinvT),
                                 n, C.byref(info))
+        del Qinv
         if rc == L.IPM_NOT_POSITIVE_DEFINITE:
             raise np.linalg.LinAlgError(f"{info.value}-th leading minor of the array is not positive definite")
         h.check(rc, h.ptr)
@@ -119,7 +121,9 @@ class LassoSolver:
             # the iteration reads
             h.check(lib.ipm_lasso_scale(h.ptr, n, n, L.dptr(self.QinvT), n, -self.m * self.rho, 1.0, 0), h.ptr)
             self.Qs = self._blocked(self.QinvT)
+            self.QinvT = None           # the blocked copy is all the iteration reads from here on
         else:
+            self._Qs_chunks = None      # the chunks' blocked Qs, built at the first solve
             self.solve_func = self._run_admm_chunks
 
     # ---------------------------------------------------------------------------------------
@@ -224,12 +228,17 @@ class LassoSolver:
         self.solutions = np.empty(self.num_samples)
         reg_is_array = isinstance(self.reg, np.ndarray)
         n = self.n
-        Qs = torch.empty((n, n), dtype=torch.float64, device=self.dev)
-        self.h.check(self.lib.ipm_copy(self.h.ptr, L.dptr(Qs), L.dptr(self.QinvT), n * n), self.h.ptr)
-        # Qinv_cache * -self.m * self.rho, left to right (LassoSolver.py:386)
-        self.h.check(self.lib.ipm_lasso_scale(self.h.ptr, n, n, L.dptr(Qs), n, float(-self.m), float(self.rho), 1),
-                     self.h.ptr)
-        Qs = self._blocked(Qs)
+        key = (self.m, float(self.rho))
+        if self._Qs_chunks is None or self._Qs_chunks[0] != key:
+            # Qinv_cache * -self.m * self.rho, left to right (LassoSolver.py:386): built once per
+            # (m, rho) and reused by every solve
+            Qs = torch.empty((n, n), dtype=torch.float64, device=self.dev)
+            self.h.check(self.lib.ipm_copy(self.h.ptr, L.dptr(Qs), L.dptr(self.QinvT), n * n), self.h.ptr)
+            self.h.check(self.lib.ipm_lasso_scale(self.h.ptr, n, n, L.dptr(Qs), n, float(-self.m), float(self.rho),
+                                                  1), self.h.ptr)
+            self._Qs_chunks = (key, self._blocked(Qs))
+            del Qs
+        Qs = self._Qs_chunks[1]
         gaps_dev = torch.zeros((self.max_iters, self.num_samples), dtype=torch.float64, device=self.dev) \
             if self.compute_loss else None
         indices = np.array(range(self.b.shape[1]))

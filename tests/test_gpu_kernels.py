@@ -156,24 +156,29 @@ def test_potrf_ragged_rows(n, ncols, monkeypatch):
 def test_potrf_split_trailing_tiles(n, ncols, monkeypatch):
     """Trailing tiles of a launch's last round split in two K halves (IPM_SPLIT, default on; the
     upper half's partial tile handed over through the workspace), on the C-burst tile loop
-    (IPM_LAZYC=0: the default keeps lazy-eligible launches whole), and the lazy-C default: the
-    factors agree with the unsplit one to fp64 rounding and with torch's Cholesky to 1e-10."""
+    (IPM_LAZYC=0: the default keeps lazy-eligible launches whole), the lazy-C loop for K = 256
+    tiles only (IPM_LAZYC=1), and the library default (IPM_LAZYC unset: K = 512 pair tiles lazy
+    too): the factors agree with the unsplit one to fp64 rounding and with
+    torch's Cholesky to 1e-10."""
     import torch
     from gpu_util import potrf as P
     g = torch.Generator(device="cuda").manual_seed(n + 1)
     M = torch.rand((n + 5, n), dtype=torch.float64, device="cuda", generator=g) - 0.5
     A = M.T @ M + n * torch.eye(n, dtype=torch.float64, device="cuda")
     out = {}
-    for mode, lazy in (("0", "0"), ("1", "0"), ("1", "1")):
+    for mode, lazy in (("0", "0"), ("1", "0"), ("1", "1"), ("1", "default")):
         monkeypatch.setenv("IPM_SPLIT", mode)
-        monkeypatch.setenv("IPM_LAZYC", lazy)
+        if lazy == "default":
+            monkeypatch.delenv("IPM_LAZYC", raising=False)
+        else:
+            monkeypatch.setenv("IPM_LAZYC", lazy)
         H = A.clone()
         rc, info = P(H, n, n, ncols=ncols)
         assert rc == 0 and info == 0
         out[mode + lazy] = torch.tril(H.T)[:, :ncols]
     scale = out["00"].abs().max()
     L11 = torch.linalg.cholesky(A[:ncols, :ncols])
-    for k in ("10", "11"):
+    for k in ("10", "11", "1default"):
         d = ((out[k] - out["00"]).abs().max() / scale).item()
         print(f"n={n}: split {k[0]} lazy {k[1]} vs unsplit max rel {d:.2e}")
         assert d < 1e-12
@@ -209,12 +214,15 @@ def test_getrf_getrs_match_numpy(n):
 
 @pytest.mark.parametrize("n,rank,nrhs,indef", [(50, 50, 1, False), (200, 120, 3, False), (300, 90, 1, True),
                                                (301, 90, 1, False), (1024, 700, 1, False), (1025, 1025, 1, False),
-                                               (1025, 700, 2, False)])
+                                               (1025, 700, 2, False), (257, 257, 1, False),
+                                               (1000, 1000, 16, True), (2048, 1500, 64, False)])
 def test_lstsq_sym_matches_numpy(n, rank, nrhs, indef):
     """Minimum-norm least squares (ipm_lstsq_sym: eigenvectors, gelsd's rcond = eps*n cut) vs
     np.linalg.lstsq(H, B, rcond=None) -- the np_lstsq method and the Cholesky-failure backup
     (NewtonSolver.py:212-227, 334-341).  Rank-deficient H (PSD, or indefinite) is where it differs
-    from an LU solve; B row-major n x nrhs."""
+    from an LU solve; B row-major n x nrhs.  n <= 256: the one-workgroup Jacobi; above, the blocked
+    Jacobi (32-index blocks, odd block counts padded: n = 257, 301, 1025); nrhs >= 8 applies the
+    pseudo-inverse through the MFMA GEMM."""
     import ctypes
     import torch
     from gpu_util import handle
@@ -357,12 +365,9 @@ def test_potrf_wait_bound_fails_loudly():
 
 
 @pytest.mark.parametrize("n,ncols", [(130, 129), (200, 200), (1030, 1030), (2049, 2048), (4097, 4096), (8193, 8192)])
-def test_potrf_diag_role2(n, ncols, monkeypatch):
-    """The round-4 diagonal role (ipm_diag2.h: one sweep solves the whole 16-column block column and
-    L_JJ^-1; two barriers per step), forced with IPM_DIAG2=1 on full and partial last panels and on
-    the bordered Newton layout (ncols = n - 1): the factor against NumPy's, the rows below it
-    against L21 = A21 L11^-T."""
-    monkeypatch.setenv("IPM_DIAG2", "1")
+def test_potrf_partial_and_bordered(n, ncols):
+    """The fused Cholesky on full and partial last panels and on the bordered Newton layout
+    (ncols = n - 1): the factor against NumPy's, the rows below it against L21 = A21 L11^-T."""
     rng = np.random.default_rng(n + 3 * ncols)
     M = rng.normal(size=(n + 5, n))
     A = M.T @ M + n * np.eye(n)
@@ -377,12 +382,10 @@ def test_potrf_diag_role2(n, ncols, monkeypatch):
         np.testing.assert_allclose(got[ncols:, :ncols], L21, rtol=1e-10, atol=1e-10 * np.abs(L21).max())
 
 
-@pytest.mark.parametrize("diag2", ["0", "1"])
-def test_potrf_not_pd_info_matches_lapack(diag2, monkeypatch):
-    """A non-positive pivot inside a diagonal role: LAPACK's info (first failing column, 1-based)
-    with either role, and the factorization ends (every later launch sees the failure word)."""
+def test_potrf_not_pd_info_matches_lapack():
+    """A non-positive pivot inside a diagonal role: LAPACK's info (first failing column, 1-based),
+    and the factorization ends (every later launch sees the failure word)."""
     import scipy.linalg
-    monkeypatch.setenv("IPM_DIAG2", diag2)
     n = 1030
     rng = np.random.default_rng(21)
     M = rng.normal(size=(n + 5, n))

@@ -169,6 +169,36 @@ def test_m3_truncated_trajectory(name):
         assert nd_x <= 1.0, nd_x
 
 
+@pytest.mark.parametrize("timing", [0, 1])
+def test_m3_phase1_snapshots(timing):
+    """bench.py's rank-0 evidence: the phase-1 iterate after K = 10 and K = 30 Newton
+    steps against the reference's snapshots x_snap_K (m3_qp_full), with the engine's HIP-event
+    timing mode (ipm_set_timing, what the bench runs under) off and on.  Both must give the same
+    iterate bit for bit, within 1e-6 of the reference."""
+    z = _fixture("m3_qp_full")
+    spec, kw = _instance(z)
+    out = {}
+    for K in (10, 30):
+        s = _cls(spec)(check_cvxpy=False, suppress_print=True, **kw)
+        if timing:
+            h = s.phase1_solver.phase1_fm.prob.handle
+            h.lib.ipm_set_timing(h.ptr, 1)
+        s.solve(iteration_budget=K)
+        if timing:
+            h.lib.ipm_set_timing(h.ptr, 0)
+        steps, _ = _device_trace(s)
+        x = s.phase1_solver.x.cpu().numpy()
+        err = rel(x, z[f"x_snap_{K}"])
+        out[K] = x
+        print(f"[timing={timing}] K={K}: x rel {err:.2e}, steps identical "
+              f"{np.array_equal(steps, z['trace_step'][:len(steps)])}")
+        assert np.array_equal(steps, z["trace_step"][:len(steps)])
+        assert err <= XSTAR_RTOL, err
+    np.save(f"/tmp/ipm_ph1_snap_t{timing}.npy", np.stack([out[10], out[30]]))
+    if timing and os.path.exists("/tmp/ipm_ph1_snap_t0.npy"):
+        np.testing.assert_array_equal(np.load("/tmp/ipm_ph1_snap_t0.npy"), np.stack([out[10], out[30]]))
+
+
 @pytest.mark.parametrize("name", ["m2_qp", "m3_qp_ph1", "m3_qp_feas", "m3_lp"])
 def test_linesearch_flip_rate(name, monkeypatch):
     """The 64-candidate table line search against the reference-exact one (IPM_LINESEARCH=compare:

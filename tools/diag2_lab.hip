@@ -9,11 +9,14 @@
 #include <cstdio>
 #include <vector>
 #include "../interiorpoint-gpu_amd/csrc/ipm_blas.hip"
+namespace ipm {
+#include "../interiorpoint-gpu_amd/csrc/ipm_diag2.h"   // lab-only: not part of the library kernel
+}
 
 template <int ROLE>
 __global__ __launch_bounds__(256, 2) void k_lab(double* A, int64_t lda, double* ws, unsigned* ctl, int* info,
                                                 unsigned long long* cyc) {
-  __shared__ ipm::BlockSmem sm;
+  __shared__ union { ipm::DiagSmem d; ipm::Diag2Smem d2; } sm;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   if (ROLE == 0) ipm::diag_role<true, 130>(0, 128, A, lda, ws, info, ws + ipm::PF_DINV, &ctl[1], sm.d, &ctl[4]);
   else if (ROLE == 1) ipm::diag_role2<true, 0>(0, 128, A, lda, ws, info, ws + ipm::PF_DINV, &ctl[1], sm.d2, &ctl[4]);
