@@ -230,6 +230,12 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
       return;
     }
   }
+  // super-block tile order (tri_sb_index; IPM_SYRK_SB = block size in tiles, 0 = row order)
+  static const int sb = [] { const char* v = getenv("IPM_SYRK_SB"); return v ? atoi(v) : 0; }();
+  if (sb > 0) {
+    a.sb = sb;
+    a.xcd_remap = 0;   // (tri_sb_index applies the XCD-contiguous runs itself)
+  }
   if (e.split_ws) mfma_gemm_launch_split(st, a, e.split_ws, e.split_cap, 2 * num_cus());
   else mfma_gemm_launch(st, a);
 }

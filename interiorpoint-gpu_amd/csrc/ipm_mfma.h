@@ -70,7 +70,45 @@ struct GemmArgs {
   int64_t ldc2 = 0, n2 = 0, n2c = 0;   // C2 rows / columns (relative to the tile origin)
   int xbal = 0;                  // blockIdx b -> tile xb[b % 8] + b / 8 (runs of equal work per XCD)
   int xb[9] = {};
+  int sb = 0;                    // tri grids (KKT SYRK): super-block order, sb x sb tiles (0: row order);
+                                 // applied by the kernels before mfma_tile (tri_sb_index), xcd_remap = 0
 };
+
+// Super-block order of a lower-triangle tile grid (GemmArgs::sb = S): the XCD-contiguous run of
+// enumeration index Lw (the same remap as xcd_remap), then super-rows of S tile rows in order,
+// inside a super-row the S x S blocks left to right (row-major inside a block) and the triangular
+// diagonal block last.  The 2 x 32 workgroups an XCD runs at once then cover one S = 8 block: 8 X
+// and 8 Y operand panels between them instead of 1 X panel and 64 Y panels (the row order's tile
+// run), so the panels' slabs are L2 hits.  Returns the plain row-order index bi (bi + 1) / 2 + bj
+// that mfma_tile / tile_ij decode.  A bijection on [0, nblk).
+__device__ __forceinline__ int64_t tri_sb_index(const GemmArgs& a, int64_t Lw) {
+  const int64_t S = a.sb, T = a.tiles_i, q = a.nblk >> 3;
+  int64_t L = Lw;
+  if (L < (q << 3)) L = (L & 7) * q + (L >> 3);
+  int64_t Bi = 0, base = 0, r = 0;
+  for (;;) {
+    r = std::min<int64_t>(S, T - S * Bi);
+    const int64_t cnt = Bi * r * S + r * (r + 1) / 2;
+    if (L < base + cnt || r <= 0) break;
+    base += cnt;
+    ++Bi;
+  }
+  const int64_t u = L - base;
+  int64_t bi, bj;
+  if (u < Bi * r * S) {
+    const int64_t Bj = u / (r * S), v = u - Bj * r * S;
+    bi = S * Bi + v / S;
+    bj = S * Bj + v % S;
+  } else {
+    const int64_t w = u - Bi * r * S;
+    int64_t row = (int64_t)((sqrt(8.0 * (double)w + 1.0) - 1.0) * 0.5);
+    while ((row + 1) * (row + 2) / 2 <= w) ++row;
+    while (row * (row + 1) / 2 > w) --row;
+    bi = S * Bi + row;
+    bj = S * Bi + (w - row * (row + 1) / 2);
+  }
+  return bi * (bi + 1) / 2 + bj;
+}
 
 // agent-coherent (sc1) element access: data handed between workgroups of ONE launch
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -587,7 +625,8 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
     if (s0 + l < s1) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, s0 + l, sm);
     return;
   }
-  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
+  for (int64_t Lb = blockIdx.x; Lb < a.nblk; Lb += gridDim.x) {
+    const int64_t Lw = a.sb ? tri_sb_index(a, Lb) : Lb;
     if (BM_ == 128 && VEC && WJ == 2 && tile_fast_ok<BM_>(a, Lw))
       mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, false, (BM_ == 128 && VEC && WJ == 2) ? 1 : 0>(a, Lw, sm);
     else
@@ -609,16 +648,18 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t 
   const int64_t b = blockIdx.x;
   constexpr int FL = (BM_ == 128 && VEC) ? 1 : 0;
   if (b < s_full) {
-    if (FL && tile_fast_ok<BM_>(a, b)) mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, b, sm);
-    else mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, b, sm);
+    const int64_t Lw = a.sb ? tri_sb_index(a, b) : b;
+    if (FL && tile_fast_ok<BM_>(a, Lw)) mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, Lw, sm);
+    else mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, Lw, sm);
     return;
   }
   const int64_t u = b - s_full, p = u >> 1;
   double* part = sscr + p * (int64_t)(BM_ * BM_);
-  if (FL && (a.K % 32) == 0 && tile_fast_ok<BM_>(a, s_full + p))
-    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, s_full + p, sm, (u & 1) ? 2 : 1, part, sflag + p);
+  const int64_t Lw = a.sb ? tri_sb_index(a, s_full + p) : s_full + p;
+  if (FL && (a.K % 32) == 0 && tile_fast_ok<BM_>(a, Lw))
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
   else
-    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, s_full + p, sm, (u & 1) ? 2 : 1, part, sflag + p);
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
 }
 
 // Stream-K tail (the KKT SYRK on 128-tiles): a lower-triangle grid of nt = R * slots + q tiles
@@ -669,12 +710,12 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
     whole = b >= npc;
   }
   if (whole) {
-    const int64_t L = pieces_last ? b : b - npc;
+    const int64_t L = a.sb ? tri_sb_index(a, pieces_last ? b : b - npc) : (pieces_last ? b : b - npc);
     if (FL && tile_fast_ok<BM>(a, L)) mfma_tile<BM, WEIGHT, VEC, 2, false, false, true, FL>(a, L, sm);
     else mfma_tile<BM, WEIGHT, VEC, 2, false, false, true>(a, L, sm);
     return;
   }
-  const int64_t ti = b / P, p = b - ti * P, L = s_full + ti;
+  const int64_t ti = b / P, p = b - ti * P, L = a.sb ? tri_sb_index(a, s_full + ti) : s_full + ti;
   const int64_t k0 = p * Kp, k1 = std::min<int64_t>(a.K, k0 + Kp);
   double* part = sscr + b * (int64_t)(BM * BM);
   // (the flag mfma_tile raises after its partial: a per-piece word past the tile counters)

@@ -1,11 +1,11 @@
 #!/bin/bash
-# One GPU-box pass: build, GPU tests, default bench line, rocprofv3 kernel-trace summary, and the
+# One GPU-box pass (the library is built in-tree beforehand, on the CPU side): GPU tests, default bench line, rocprofv3 kernel-trace summary, and the
 # PMC passes (FETCH_SIZE / WRITE_SIZE / MFMA busy cycles, each in its own run) for the two MFMA
 # kernels.  Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 OUT=gpurun_out/${TAG:-r2}
 mkdir -p $OUT
-make -j8 > $OUT/build.log 2>&1 || { echo "build failed"; tail -20 $OUT/build.log; exit 1; }
+# (the library is built in-tree on the CPU side; nothing is compiled on the box)
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 ${TT:-900} python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread ${PYTEST_ARGS} > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -3 $OUT/pytest_gpu.log
