@@ -191,14 +191,15 @@ __global__ __launch_bounds__(1024) void k_jacobi_wg(int n, double* A, int64_t ld
 // ---------------------------------------------------------------------------------------------
 // Large n: BLOCKED two-sided Jacobi.  The index range is cut into nb = ceil(n / 32) blocks of 32
 // (an odd count gets one empty block); every round pairs the blocks by the same circle ordering
-// and, for each pair (P, Q), diagonalises the 64 x 64 subproblem S = A[P u Q, P u Q] completely
+// and, for each pair (P, Q), rotates the 64 x 64 subproblem S = A[P u Q, P u Q] by one cyclic sweep
 // (k_bj_eig: the cyclic Jacobi above, in LDS, one workgroup per pair) into S' = G^T S G.  The
 // orthogonal G (64 x 64) is then applied to the whole matrix on MFMA tiles -- rows
 // A[P u Q, :] <- G^T A[P u Q, :] (k_bj_rows), then columns A[:, P u Q] <- A[:, P u Q] G and
 // V[:, P u Q] <- V[:, P u Q] G (k_bj_cols) -- and the pair's own 64 x 64 block is replaced by the
-// diagonalised S' (whose rotated entries are exact zeros, like the 2 x 2 form's).  A sweep is
+// rotated S' (whose rotated entries are exact zeros, like the 2 x 2 form's).  A sweep is
 // nb - 1 rounds; the sweeps stop when no subproblem rotated anything (the same per-entry tests as
-// the 2 x 2 method, so the stopping rule and the answer are the same).  Work per sweep ~12 n^3
+// the 2 x 2 method, so the stopping rule and the answer are the same; a sweep of the outer loop is
+// the convergence unit, JMAX_SWEEPS of them without convergence sets the info word).  Work per sweep ~12 n^3
 // flops on MFMA instead of n - 1 rounds of scattered 2 x 2 updates over all of A and V; a pair
 // whose subproblem did not rotate (most of them in the last sweeps) skips its updates.
 constexpr int BJ = 32;         // block size
@@ -212,8 +213,7 @@ __device__ __forceinline__ int64_t bj_index(int P, int Q, int k) {
 // per-pair scratch: G (BS x BS, column-major) | S' (BS x BS) ; rot flags (one int per pair)
 __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const double* __restrict__ A, int64_t lda,
                                                 const double* frob2, double* __restrict__ gbuf,
-                                                int* __restrict__ rflag, int* __restrict__ nrot,
-                                                int* __restrict__ info) {
+                                                int* __restrict__ rflag, int* __restrict__ nrot, int inner) {
   __shared__ double S[BS * BLD], G[BS * BLD];
   __shared__ double sc[BS / 2], ss[BS / 2];
   __shared__ int sp[BS / 2], sq[BS / 2];
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
   const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
   int total = 0, sweep = 0;
   __syncthreads();
-  for (; sweep < JMAX_SWEEPS; ++sweep) {
+  for (; sweep < inner; ++sweep) {
     if (tid == 0) srot = 0;
     __syncthreads();
     for (int rr = 0; rr < BS - 1; ++rr) {
@@ -293,7 +293,6 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
   if (tid == 0) {
     rflag[pair] = total > 0 ? 1 : 0;
     if (total > 0) atomicAdd(nrot, total);
-    if (sweep >= JMAX_SWEEPS) *info = 1;   // sticky: never cleared here
   }
 }
 
@@ -462,6 +461,13 @@ static std::atomic<int> g_fail_call{-1};
 void set_lstsq_fail_call(int k) { g_fail_call.store(k); }
 __global__ void k_set_flag(int* p) { *p = 1; }
 
+// inner cyclic sweeps per subproblem and round (IPM_BJ_INNER, default 1): the subproblem need not
+// be diagonalised completely -- every index pair is still rotated in every outer sweep, and the
+// outer stopping rule (a sweep without any rotation) is unchanged, so is the answer's accuracy
+static int bj_inner_sweeps() {
+  static const int v = [] { const char* e = getenv("IPM_BJ_INNER"); return e ? std::max(1, atoi(e)) : 1; }();
+  return v;
+}
 static inline int64_t bj_pairs(int64_t n) {
   const int64_t nb = (n + BJ - 1) / BJ;
   return (nb + (nb & 1)) / 2;
@@ -498,7 +504,7 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
       hipMemsetAsync(nrot, 0, sizeof(int), st);
       for (int r = 0; r < (int)nbp - 1; ++r) {
         hipLaunchKernelGGL(k_bj_eig, dim3((unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A, lda, frob2, gbuf,
-                           rflag, nrot, info_dev);
+                           rflag, nrot, bj_inner_sweeps());
         hipLaunchKernelGGL(k_bj_rows, dim3((unsigned)tiles, (unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A,
                            lda, gbuf, rflag);
         hipLaunchKernelGGL(k_bj_cols, dim3((unsigned)tiles, (unsigned)np, 2), dim3(256), 0, st, (int)n, (int)nbp, r,
