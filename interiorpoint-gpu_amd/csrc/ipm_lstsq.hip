@@ -34,6 +34,8 @@
 #include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "ipm_common.h"
@@ -514,6 +516,8 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
       if (hipMemcpyAsync(&h, nrot, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipStreamSynchronize(st) != hipSuccess)
         return -1;
+      static const bool dbg = getenv("IPM_BJ_DEBUG") != nullptr;
+      if (dbg) fprintf(stderr, "blocked Jacobi n=%ld sweep %d: %d rotations\n", (long)n, sweep, h);
       if (h == 0) break;
     }
     if (sweep >= JMAX_SWEEPS) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, st, info_dev);   // sticky
