@@ -286,9 +286,11 @@ def main():
     if args.concurrent:
         # each instance = its own stream; HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues
         # (4 by default) -- streams sharing a queue serialise.  Must be set before the HIP runtime
-        # starts (the box presets 4: override it, <= 32 allowed).
+        # starts (the box presets 4: override it, <= 32 allowed).  8 x n=2048 (config 4): 4 queues
+        # 1610, 8 queues 2231-2279, 16 queues 1645-2142, 32 queues 869 it/s (profiles/r4f, r4g) --
+        # more concurrent kernels than that fill the CUs with waiting Cholesky roles.
         from ipm355 import dist as _D
-        _D.configure_queues(int(os.environ.get("IPM_HW_QUEUES", "16")))
+        _D.configure_queues(int(os.environ.get("IPM_HW_QUEUES", "8")))
 
     import torch
     import torch.distributed as dist

@@ -1126,7 +1126,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_panel(int64_t n, int64_t k0, i
                                                      double* __restrict__ A, int64_t lda, double* ws, unsigned* ctl,
                                                      int* __restrict__ info) {
   __shared__ DiagSmem sm;
-  __shared__ int sticket, sflag, sexh;
+  __shared__ int sticket, sflag;
   if (threadIdx.x == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
   __syncthreads();
   const int t = sticket;
@@ -1229,12 +1229,6 @@ struct BlockArgs {
   int64_t sa = 0, sb = 0;
   int rpad_a = 0, rpad_b = 0;
   int rowprio = 0;              // s_setprio of the non-critical row chunks (IPM_ROWPRIO)
-  // persistent trailing-tile workers (IPM_SPERSIST=1): nstk S tickets (<= the workgroup slots), each
-  // worker runs tiles from the per-XCD queues (xcd_tile over the ns tiles) until they are empty, so
-  // that one tile's store epilogue drains under the next tile's loads and MFMAs instead of every
-  // workgroup of a round finishing -- and storing -- at once.  Otherwise nstk = ns.
-  int persist = 0;
-  int64_t nstk = 0;
 };
 #ifndef FLEX_PROG
 #define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
@@ -1311,10 +1305,10 @@ struct RoleTrace {
 // LAZY (default; IPM_LAZYC=0 turns it off.  FASTS launches whose trailing tiles are all whole K = 256 tiles, no strips or
 // K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
 // before the first MFMA
-template <bool VEC, bool FASTS = false, int LAZY = 0, bool PERS = false>
+template <bool VEC, bool FASTS = false, int LAZY = 0>
 __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   __shared__ BlockSmem sm;
-  __shared__ int sticket, sflag, sexh;
+  __shared__ int sticket, sflag;
   const int tid = threadIdx.x;
   if (tid == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
   unsigned* const failw = &b.ctl[CTL_FAIL];
@@ -1469,10 +1463,10 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
           pb = true;
           chunk = t;
         }
-      } else if ((t -= b.nrb + b.rpad_b) < b.nstk - b.sb) {
+      } else if ((t -= b.nrb + b.rpad_b) < b.ns - b.sb) {
         kind = K_TILE;
         t += b.sb;
-      } else if ((t -= b.nstk - b.sb) < b.gs_total) {
+      } else if ((t -= b.ns - b.sb) < b.gs_total) {
         kind = K_GS;   // last: they fill the CUs the chain leaves idle
       }
     }
@@ -1653,18 +1647,12 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   }
   if (kind == K_TILE) {
     ROLE(4);
-    // persistent workers (b.persist): the whole tile step again with the next queued tile, until
-    // the XCD queues are empty
-#pragma nounroll
-    for (;;) {
     // A trailing tile that lands on the CU of a running critical-path role hands its tile to
     // that role's spill word and sleeps, keeping the slot so that no MFMA tile shares the CU with
     // the chain.  Every tile workgroup, after its own tile, takes what is in the spill words; the
     // sleeper, once the role is done, runs its tile itself if nobody took it.
     if (tid == 0) {
-      // this workgroup's (first) tile: its XCD's run (-1: the queues are empty)
-      if (b.s_map == 2 || PERS) t = xcd_tile(&b.ctl[CTL_XQ], b.ns);
-      if (PERS) sexh = t < 0;
+      if (b.s_map == 2) t = xcd_tile(&b.ctl[CTL_XQ], b.ns);   // this workgroup's tile: its XCD's run
       const unsigned me = 1u + cu_key();
       int q = -1;
       for (int i = 0; i < NCRIT && q < 0; ++i)
@@ -1716,11 +1704,6 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
                      : b.f0 + (u < 0 ? st : b.s_full + p),
             sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p, -1, -1, b.info, failw);
       }
-    }
-    if (!PERS) break;
-    const int ex = sexh;   // (read by every thread before thread 0 writes it again)
-    __syncthreads();
-    if (ex) break;
     }
   }
 }
@@ -1939,9 +1922,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   const bool lazy_on = !(elz && elz[0] == '0');
   const bool lazy2_on = lazy_on && !(elz && elz[0] == '1');   // IPM_LAZYC=1: K = 256 tiles only
   PairPlan pl = potrf_pair_plan(n, ncols, nblocks, defer);
-  // IPM_SPERSIST=1: persistent trailing-tile workers (BlockArgs::persist; read per call: A/B tests)
-  const char* eper = getenv("IPM_SPERSIST");
-  const bool persist_on = eper && eper[0] == '1';
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     const int kind = pl.kind[bk];
     const int64_t Kla = kind == 2 ? 2 * CH_NB : CH_NB;   // look-ahead depth (EVEN: the pair)
@@ -2143,7 +2123,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     // (LAZY 2: the block pairs' K = 512 tiles, strips included)
     const bool lazy_cand = lazy_on && fasts_on && vec && (b.s.ni % 128) == 0 &&
                            ((b.s.K == CH_NB && b.nstrip == 0) || (lazy2_on && b.s.K == 2 * CH_NB));
-    const bool split_here = split_on && !lazy_cand && !persist_on;
+    const bool split_here = split_on && !lazy_cand;
     if (b.s_full > 0 && !defer && (split_here || rowpos_on)) {
       // the planner's split count and row positions (cached per size and block: they depend on
       // nothing else)
@@ -2194,15 +2174,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     }
     static const int rowprio = [] { const char* e = getenv("IPM_ROWPRIO"); return e ? atoi(e) : 0; }();
     b.rowprio = rowprio;
-    b.nstk = b.ns;
-    if (persist_on && vec && b.ns > 0 && !defer && !flex_on && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0) {
-      // persistent trailing-tile workers: at most one per workgroup slot; the rows follow them
-      b.persist = 1;
-      b.s.xcd_remap = 0;   // (xcd_tile hands out tri-order indices in XCD-contiguous runs)
-      b.nstk = std::min<int64_t>(b.ns, 2 * num_cus());
-      b.sa = b.sb = b.nstk;
-      b.rpad_a = b.rpad_b = 0;
-    }
     if (defer) {
       // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
       b.gX = ds->X;
@@ -2230,7 +2201,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     // (IPM_FLEX=1: measured slower, 6.52 -> 7.14 ms at n = 8192 -- row chunks started beside the
     // MFMA tiles run far slower than at the launch's end; kept as a knob)
     b.flex = flex_on ? 1 : 0;
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.nstk + b.gs_total +
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total +
                          b.rpad_a + b.rpad_b;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
@@ -2239,13 +2210,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     const bool lazy = lazy_on && fasts && b.s.K == CH_NB && b.nstrip == 0 && b.s_full == b.ns;
     const bool lazy2 = lazy2_on && fasts && b.s.K == 2 * CH_NB && b.nstrip + b.s_full == b.ns &&
                        (b.nstrip == 0 || b.s2.K == 2 * CH_NB) && (b.nrag == 0 || b.rag_K <= 2 * CH_NB);
-    if (b.persist && vec && lazy)
-      hipLaunchKernelGGL((k_potrf_block<true, true, 1, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (b.persist && vec && lazy2)
-      hipLaunchKernelGGL((k_potrf_block<true, true, 2, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (b.persist && vec && fasts)
-      hipLaunchKernelGGL((k_potrf_block<true, true, 0, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, 1>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, 1>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec && lazy2) hipLaunchKernelGGL((k_potrf_block<true, true, 2>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
     else if (vec) hipLaunchKernelGGL((k_potrf_block<true, false>), dim3((unsigned)grid), dim3(256), 0, st, b);

@@ -351,18 +351,65 @@ __global__ __launch_bounds__(256) void k_bj_rows(int n, int nbp, int r, double* 
   }
 }
 
+// A <- J^T A J in ONE pass: the tile of A on pair I's rows and pair J's columns (64 x 64, the same
+// pairing on both sides) becomes G_I^T T G_J -- A is read and written once per round instead of
+// twice (a row pass, then a column pass).  The pair's own tile (I == J) takes the rotated S'.  A
+// pair that did not rotate has G = I exactly, so its product is exact (no skip needed for one side).
+__global__ __launch_bounds__(256) void k_bj_tile(int n, int nbp, int r, double* __restrict__ A, int64_t lda,
+                                                 const double* __restrict__ gbuf, const int* __restrict__ rflag) {
+  const int I = blockIdx.x, J = blockIdx.y;
+  if (!rflag[I] && !rflag[J]) return;
+  __shared__ double Gl[BS * BLD], T[BS * BLD];
+  int a, b;
+  circle_pair(nbp, r, I, a, b);
+  const int PI = min(a, b), QI = max(a, b);
+  circle_pair(nbp, r, J, a, b);
+  const int PJ = min(a, b), QJ = max(a, b);
+  const int tid = threadIdx.x;
+  const double* gI = gbuf + (int64_t)I * 2 * BS * BS;
+  if (I == J) {
+    const double* sfin = gI + BS * BS;
+    for (int e = tid; e < BS * BS; e += 256) {
+      const int i = e % BS, j = e / BS;
+      const int64_t gi = bj_index(PI, QI, i), gj = bj_index(PJ, QJ, j);
+      if (gi < n && gj < n) A[gj * lda + gi] = sfin[e];
+    }
+    return;
+  }
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int k = e % BS, j = e / BS;
+    Gl[j * BLD + k] = gI[e];   // G_I(k, j)
+    const int64_t gi = bj_index(PI, QI, k), gj = bj_index(PJ, QJ, j);
+    T[j * BLD + k] = (gi < n && gj < n) ? A[gj * lda + gi] : 0.0;   // T(k, j)
+  }
+  __syncthreads();
+  // T <- G_I^T T : D(i, j) = sum_k G_I(k, i) T(k, j)
+  bj_tile([&](int i, int k) { return Gl[i * BLD + k]; }, [&](int k, int j) { return T[j * BLD + k]; }, T);
+  const double* gJ = gbuf + (int64_t)J * 2 * BS * BS;
+  for (int e = tid; e < BS * BS; e += 256) Gl[(e / BS) * BLD + e % BS] = gJ[e];   // G_J(k, j)
+  __syncthreads();
+  // T <- T G_J : D(i, j) = sum_k T(i, k) G_J(k, j)
+  bj_tile([&](int i, int k) { return T[k * BLD + i]; }, [&](int k, int j) { return Gl[j * BLD + k]; }, T);
+  for (int e = tid; e < BS * BS; e += 256) {
+    const int i = e % BS, j = e / BS;
+    const int64_t gi = bj_index(PI, QI, i), gj = bj_index(PJ, QJ, j);
+    if (gi < n && gj < n) A[gj * lda + gi] = T[j * BLD + i];
+  }
+}
+
 // columns: M[r0 : r0 + 64, P u Q] <- M[r0 : r0 + 64, P u Q] G for M = A (z = 0) and V (z = 1);
 // in A the pair's own rows take the diagonalised S' instead
 __global__ __launch_bounds__(256) void k_bj_cols(int n, int nbp, int r, double* __restrict__ A, int64_t lda,
                                                  double* __restrict__ V, int64_t ldv,
-                                                 const double* __restrict__ gbuf, const int* __restrict__ rflag) {
+                                                 const double* __restrict__ gbuf, const int* __restrict__ rflag,
+                                                 int vonly) {
   const int pair = blockIdx.y;
   if (!rflag[pair]) return;
   __shared__ double Gl[BS * BLD], Y[BS * BLD];
   int a, b;
   circle_pair(nbp, r, pair, a, b);
   const int P = min(a, b), Q = max(a, b), tid = threadIdx.x;
-  const bool isA = blockIdx.z == 0;
+  const bool isA = !vonly && blockIdx.z == 0;
   double* M = isA ? A : V;
   const int64_t ld = isA ? lda : ldv;
   const int64_t r0 = (int64_t)blockIdx.x * BS;
@@ -470,6 +517,11 @@ static int bj_inner_sweeps() {
   static const int v = [] { const char* e = getenv("IPM_BJ_INNER"); return e ? std::max(1, atoi(e)) : 1; }();
   return v;
 }
+// IPM_BJ_FUSED=0: the two-pass A update (rows, then columns) instead of the one-pass tile update
+static bool bj_fused() {
+  static const bool v = [] { const char* e = getenv("IPM_BJ_FUSED"); return !(e && e[0] == '0'); }();
+  return v;
+}
 static inline int64_t bj_pairs(int64_t n) {
   const int64_t nb = (n + BJ - 1) / BJ;
   return (nb + (nb & 1)) / 2;
@@ -507,10 +559,18 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
       for (int r = 0; r < (int)nbp - 1; ++r) {
         hipLaunchKernelGGL(k_bj_eig, dim3((unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A, lda, frob2, gbuf,
                            rflag, nrot, bj_inner_sweeps());
-        hipLaunchKernelGGL(k_bj_rows, dim3((unsigned)tiles, (unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A,
-                           lda, gbuf, rflag);
-        hipLaunchKernelGGL(k_bj_cols, dim3((unsigned)tiles, (unsigned)np, 2), dim3(256), 0, st, (int)n, (int)nbp, r,
-                           A, lda, V, n, gbuf, rflag);
+        if (bj_fused()) {
+          // A in one tile pass, V's columns in the column kernel (z = 1 only)
+          hipLaunchKernelGGL(k_bj_tile, dim3((unsigned)np, (unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A,
+                             lda, gbuf, rflag);
+          hipLaunchKernelGGL(k_bj_cols, dim3((unsigned)tiles, (unsigned)np, 1), dim3(256), 0, st, (int)n, (int)nbp, r,
+                             A, lda, V, n, gbuf, rflag, 1);
+        } else {
+          hipLaunchKernelGGL(k_bj_rows, dim3((unsigned)tiles, (unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A,
+                             lda, gbuf, rflag);
+          hipLaunchKernelGGL(k_bj_cols, dim3((unsigned)tiles, (unsigned)np, 2), dim3(256), 0, st, (int)n, (int)nbp, r,
+                             A, lda, V, n, gbuf, rflag, 0);
+        }
       }
       int h = 0;
       if (hipMemcpyAsync(&h, nrot, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -150,10 +150,13 @@ def _on(stream):
     return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
-def configure_queues(queues: int = 16) -> bool:
+def configure_queues(queues: int = 8) -> bool:
     """Give the HIP runtime `queues` hardware queues per process (GPU_MAX_HW_QUEUES, read once when
     the runtime starts) so that concurrent instances do not serialise on shared queues.  Returns
-    False when it is too late (the runtime already started); the box presets 4, gpurun allows 32."""
+    False when it is too late (the runtime already started); the box presets 4, gpurun allows 32.
+    8 is the measured best for 8 x n=2048 per GPU (config 4): 4 / 8 / 16 / 32 queues gave 1610 /
+    2231-2279 / 1645-2142 / 869 Newton it/s -- more concurrent kernels leave the CUs full of
+    Cholesky roles waiting on their chains."""
     import torch
     if torch.cuda.is_initialized():
         return False

@@ -4,6 +4,9 @@
 set -o pipefail
 OUT=gpurun_out/r4g
 mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v -s -k "lstsq" --timeout 300 --timeout-method thread > $OUT/pytest_lstsq.log 2>&1
+rc=$?; echo "pytest lstsq rc=$rc"; grep -E "lstsq n=|passed|failed|FAILED" $OUT/pytest_lstsq.log | tail -4
+[ $rc -ne 0 ] && exit $rc
 IPM_SPERSIST=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "potrf" --timeout 300 --timeout-method thread > $OUT/pytest_persist.log 2>&1
 rc=$?; echo "pytest potrf persist rc=$rc"; tail -2 $OUT/pytest_persist.log
 [ $rc -ne 0 ] && exit $rc
@@ -18,9 +21,11 @@ done 2>&1 | tee $OUT/persist_ab.txt
 L=interiorpoint-gpu_amd/ipm355/libipm355.so
 REPS=2 T=200 bash scripts/ab.sh $OUT/pab "--steps 20 --warmup 2" IPM_SPERSIST=0@$L IPM_SPERSIST=1@$L 2>&1 | tee $OUT/persist_bench_ab.txt
 [ ${PIPESTATUS[0]} -ne 0 ] && exit 1
-IPM_BJ_DEBUG=1 HOST_MAX=0 timeout -k 10 300 python scripts/lstsq_time.py 2048 8193 > $OUT/lstsq_sweeps.txt 2>&1 || exit 1
-grep -c sweep $OUT/lstsq_sweeps.txt; grep device_s $OUT/lstsq_sweeps.txt
-for r in 1 2; do
+for f in 1 0; do
+  IPM_BJ_FUSED=$f IPM_BJ_DEBUG=1 HOST_MAX=0 timeout -k 10 300 python scripts/lstsq_time.py 2048 8193 > $OUT/lstsq_sweeps_f$f.txt 2>&1 || exit 1
+  echo "fused=$f sweeps: $(grep -c sweep $OUT/lstsq_sweeps_f$f.txt)"; grep device_s $OUT/lstsq_sweeps_f$f.txt
+done
+for r in 1; do
   for q in 4 8 16; do
     IPM_HW_QUEUES=$q timeout -k 10 300 python bench.py --no-cpu --n 2048 --m 512 --instances 8 --concurrent --steps 20 --warmup 2 > $OUT/c4_q$q.json 2> $OUT/c4_q$q.err || exit 1
     python3 -c "import json;d=json.load(open('$OUT/c4_q$q.json'));print('c4 queues $q', round(d['value'],1))"
