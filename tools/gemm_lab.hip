@@ -110,7 +110,7 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm(int n, int K, const doubl
 // the LDS reads, the LDS stores and the global loads between the MFMAs; SGB = 1 also pins an
 // interleave pattern with sched_group_barrier (mask 0x008 MFMA, 0x100 DS read, 0x200 DS write,
 // 0x020 VMEM read, 0x002 VALU)
-template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+template <int BM, int BN, int WM, int WN, int BK, int TRI, int SGB>
 __global__ __launch_bounds__(WM * WN * 64) void k_gemm2(int n, int K, const double* __restrict__ X, int ldx,
                                                         const double* __restrict__ Y, int ldy,
                                                         double* __restrict__ C, int ldc, int tiles_i, int nblk) {
@@ -122,12 +122,21 @@ __global__ __launch_bounds__(WM * WN * 64) void k_gemm2(int n, int K, const doub
   __shared__ double sY[2][BK * LY];
   for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
   int bi, bj;
-  if (TRI) {
+  if (TRI == 1) {          // lower triangle, row-major tile order
     const int L = Lp;
     int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
     while ((b + 1) * (b + 2) / 2 <= L) ++b;
     while (b * (b + 1) / 2 > L) --b;
     bi = b; bj = L - b * (b + 1) / 2;
+  } else if (TRI == 2) {   // lower triangle, column-major tile order (bi fastest, as the full grid)
+    int L = Lp, c = 0;
+    while (L >= tiles_i - c) { L -= tiles_i - c; ++c; }
+    bj = c; bi = c + L;
+  } else if (TRI == 3) {   // lower triangle, column-major, each XCD a contiguous run
+    const int q = nblk >> 3;
+    int L = Lp < (q << 3) ? (Lp & 7) * q + (Lp >> 3) : Lp, c = 0;
+    while (L >= tiles_i - c) { L -= tiles_i - c; ++c; }
+    bj = c; bi = c + L;
   } else {
     bi = Lp % tiles_i; bj = Lp / tiles_i;
   }
@@ -223,12 +232,21 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_gemm4(int n, int K, const d
   __shared__ double sY[2][BK * LY];
   for (int Lp = blockIdx.x; Lp < nblk; Lp += gridDim.x) {
   int bi, bj;
-  if (TRI) {
+  if (TRI == 1) {          // lower triangle, row-major tile order
     const int L = Lp;
     int b = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
     while ((b + 1) * (b + 2) / 2 <= L) ++b;
     while (b * (b + 1) / 2 > L) --b;
     bi = b; bj = L - b * (b + 1) / 2;
+  } else if (TRI == 2) {   // lower triangle, column-major tile order (bi fastest, as the full grid)
+    int L = Lp, c = 0;
+    while (L >= tiles_i - c) { L -= tiles_i - c; ++c; }
+    bj = c; bi = c + L;
+  } else if (TRI == 3) {   // lower triangle, column-major, each XCD a contiguous run
+    const int q = nblk >> 3;
+    int L = Lp < (q << 3) ? (Lp & 7) * q + (Lp >> 3) : Lp, c = 0;
+    while (L >= tiles_i - c) { L -= tiles_i - c; ++c; }
+    bj = c; bi = c + L;
   } else {
     bi = Lp % tiles_i; bj = Lp / tiles_i;
   }
@@ -426,7 +444,7 @@ void run(const char* name, int n, int K, double* X, double* Y, double* C, double
          tot / reps, fl / best / 1e9, err / mx);
 }
 
-template <int BM, int BN, int WM, int WN, int BK, bool TRI, int SGB>
+template <int BM, int BN, int WM, int WN, int BK, int TRI, int SGB>
 void run2(const char* name, int n, int K, double* X, double* Y, double* C, double* R, int reps, int grid = 0) {
   const int ti = n / BM, tj = n / BN;
   const int nblk = TRI ? ti * (ti + 1) / 2 : ti * tj;
@@ -558,5 +576,11 @@ int main(int argc, char** argv) {
   run2<128, 128, 2, 2, 16, false, 0>("lab2 128x128 w2x2 bk16 full", n, K, X, X, C, R, reps);
   run4<128, 128, 2, 2, 16, false, 0>("lab4 reads-first full", n, K, X, X, C, R, reps);
   run4<128, 128, 2, 2, 16, false, 2>("lab4 reads-first+sb full", n, K, X, X, C, R, reps);
+  // round 4 (profiles/r4h_gemm_lab.txt): larger tiles were slower (256x128 w2x2: 53-62 TF/s,
+  // 256x128 w4x2 59.9, 128x256 54.2, 256x256 spills); the lower-triangle grid's rounds run ~16 %
+  // slower than the full grid's: tile orders of the triangle
+  run2<128, 128, 2, 2, 16, 2, 0>("lab2 tri column-major", n, K, X, X, C, R, reps);
+  run2<128, 128, 2, 2, 16, 3, 0>("lab2 tri column-major xcd runs", n, K, X, X, C, R, reps);
+  run2<128, 128, 2, 2, 16, 1, 0>("lab2 tri row-major (again)", n, K, X, X, C, R, reps);
   return 0;
 }
