@@ -555,6 +555,31 @@ void runlib(const char* name, int n, int K, bool tri, bool weight, int remap, do
          mx > 0 ? err / mx : 0.0);
 }
 
+// the library's KKT SYRK launch (mfma_gemm_launch_split: stream-K tail) with the pieces of the KKT
+// assembly switched on one at a time: the weight on k, the tP * P epilogue, the diagonal vector
+void runsyrk(const char* name, int n, int K, bool weight, bool pepi, double* X, double* C, double* w, double* P,
+             double* dv, int reps) {
+  ipm::GemmArgs a;
+  a.ni = a.nj = n; a.K = K; a.X = a.Y = X; a.ldx = a.ldy = n; a.w = weight ? w : nullptr;
+  a.C = C; a.ldc = n; a.tri = 1; a.alpha = 1.0; a.beta = 0.0;
+  if (pepi) { a.P = P; a.ldp = n; a.tP = 0.5; a.dvec = dv; }
+  const int64_t cap = ipm::syrk_split_cap(n);
+  double* ws; CK(hipMalloc(&ws, ipm::syrk_split_ws_doubles(n) * 8));
+  int ncu = 0; CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  auto L = [&]() { ipm::mfma_gemm_launch_split(0, a, ws, cap, 2 * ncu); };
+  L();
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  float best = 1e30, tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0)); L(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = std::min(best, ms); tot += ms;
+  }
+  const double fl = (double)n * (n + 1) * K;
+  printf("%-34s n=%d K=%d  best %.3f ms avg %.3f  %.1f TF/s\n", name, n, K, best, tot / reps, fl / best / 1e9);
+  CK(hipFree(ws));
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 8192;
   const int K = argc > 2 ? atoi(argv[2]) : 2048;
@@ -569,6 +594,12 @@ int main(int argc, char** argv) {
   const int reps = 5;
   double* w; CK(hipMalloc(&w, (size_t)K * 8));
   { std::vector<double> hw(K, 1.5); CK(hipMemcpy(w, hw.data(), K * 8, hipMemcpyHostToDevice)); }
+  if (argc > 3 && atoi(argv[3]) == 1) {   // the library SYRK only (IPM_STREAMK picks its tail)
+    double *P, *dv; CK(hipMalloc(&P, (size_t)n * n * 8)); CK(hipMalloc(&dv, (size_t)n * 8));
+    CK(hipMemset(P, 0, (size_t)n * n * 8)); CK(hipMemset(dv, 0, (size_t)n * 8));
+    for (int rep = 0; rep < 3; ++rep) runsyrk("lib syrk + weight + tP/dvec", n, K, true, true, X, C, w, P, dv, 8);
+    return 0;
+  }
   runlib("lib tri remap", n, K, true, false, 1, X, C, R, w, reps);
   run2<128, 128, 2, 2, 16, true, 0>("lab2 128x128 w2x2 bk16 tri", n, K, X, X, C, R, reps);
   run4<128, 128, 2, 2, 16, true, 0>("lab4 reads-first tri", n, K, X, X, C, R, reps);
@@ -579,6 +610,16 @@ int main(int argc, char** argv) {
   // round 4 (profiles/r4h_gemm_lab.txt): larger tiles were slower (256x128 w2x2: 53-62 TF/s,
   // 256x128 w4x2 59.9, 128x256 54.2, 256x256 spills); the lower-triangle grid's rounds run ~16 %
   // slower than the full grid's: tile orders of the triangle
+  {
+    double *P, *dv; CK(hipMalloc(&P, (size_t)n * n * 8)); CK(hipMalloc(&dv, (size_t)n * 8));
+    CK(hipMemset(P, 0, (size_t)n * n * 8)); CK(hipMemset(dv, 0, (size_t)n * 8));
+    for (int rep = 0; rep < 2; ++rep) {
+      runsyrk("lib syrk stream-K", n, K, false, false, X, C, w, P, dv, reps);
+      runsyrk("lib syrk stream-K + weight", n, K, true, false, X, C, w, P, dv, reps);
+      runsyrk("lib syrk stream-K + weight + tP/dvec", n, K, true, true, X, C, w, P, dv, reps);
+    }
+    CK(hipFree(P)); CK(hipFree(dv));
+  }
   run2<128, 128, 2, 2, 16, 2, 0>("lab2 tri column-major", n, K, X, X, C, R, reps);
   run2<128, 128, 2, 2, 16, 3, 0>("lab2 tri column-major xcd runs", n, K, X, X, C, R, reps);
   run2<128, 128, 2, 2, 16, 1, 0>("lab2 tri row-major (again)", n, K, X, X, C, R, reps);
