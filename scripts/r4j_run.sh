@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 4: look-ahead 32-tiles through the fold branch (fold32) A/B: HEAD library (build/abh/r4h)
+# vs this tree's with IPM_LA32F=1 / 0, then the POTRF GPU tests on this tree's library.
+set -o pipefail
+OUT=gpurun_out/r4j
+mkdir -p $OUT
+NEW=interiorpoint-gpu_amd/ipm355/libipm355.so
+for r in 1 2; do
+  for cfg in "build/abh/r4h/libipm355.so 1" "$NEW 1" "$NEW 0"; do
+    set -- $cfg
+    for n in "8193 9 8194" "4096 15"; do
+      IPM_LA32F=$2 IPM355_LIB=$PWD/$1 timeout -k 10 120 python scripts/potrf_time.py $n | sed "s|^|$1 la32f=$2 |" || exit $?
+    done
+  done
+done 2>&1 | tee $OUT/potrf_ab.txt
+[ ${PIPESTATUS[0]} -ne 0 ] && exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "potrf or chol or block" --timeout 120 --timeout-method thread > $OUT/pytest_potrf.log 2>&1
+rc=$?; echo "pytest potrf rc=$rc"; tail -3 $OUT/pytest_potrf.log
+exit $rc
