@@ -239,7 +239,9 @@ int ipm_debug_set_potrf_spin_limit(unsigned microseconds);
 int ipm_debug_lstsq_fail_call(int k);
 /* debug knob: the backward-solve workgroup holding chain ticket `ticket` sleeps ~7 ms before
    publishing its progress word (-1: off), so later tickets overtake it -- exercises the monotonic
-   progress publish.  Process-wide. */
+   progress publish.  ticket <= -2: ticket -2 - ticket sleeps before storing its x block instead,
+   so the next ticket's bounded poll of that block runs out (exercises the loud failure).
+   Process-wide. */
 int ipm_debug_set_trsv_publish_delay(int ticket);
 /* KKT-SYRK flops of one Newton step of this problem (m n (n+1) in total), split between the
    up-front SYRK kernel and the k-row slices deferred into the Cholesky launches, where they fill

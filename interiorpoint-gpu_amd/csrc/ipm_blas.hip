@@ -49,8 +49,23 @@ __global__ __launch_bounds__(256) void k_gemv_n(int64_t rows, int64_t cols, doub
     const double2* x2 = reinterpret_cast<const double2*>(x);
     double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     int64_t j = lane;
+    typedef double nt2 __attribute__((ext_vector_type(2)));
+    // two trips' loads in flight (eight per lane), folded trip by trip: the same partial sums in
+    // the same order as one trip at a time (bitwise), twice the bytes in flight per wave
+    for (; j + 448 < c2; j += 512) {
+      nt2 u[8];
+      double2 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) u[q] = __builtin_nontemporal_load(reinterpret_cast<const nt2*>(m2 + j + 64 * q));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = x2[j + 64 * q];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        a[2 * (q & 3)] = fma(u[q].x, v[q].x, a[2 * (q & 3)]);
+        a[2 * (q & 3) + 1] = fma(u[q].y, v[q].y, a[2 * (q & 3) + 1]);
+      }
+    }
     for (; j + 192 < c2; j += 256) {
-      typedef double nt2 __attribute__((ext_vector_type(2)));
       nt2 u[4];
       double2 v[4];
 #pragma unroll
@@ -2918,6 +2933,9 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
       sm.spart[q][c] = p + p2;
     }
     __syncthreads();
+    if (delay_ticket <= -2 && t == -2 - delay_ticket) {   // debug knob: a late x store (trips the
+      for (int i = 0; i < 2000; ++i) __builtin_amdgcn_s_sleep(127);   // next ticket's bounded poll)
+    }
     if (q == 0 && c < rows)
       st_sc1(y + r0 + c, (sm.spart[0][c] + sm.spart[1][c]) + (sm.spart[2][c] + sm.spart[3][c]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -122,15 +122,27 @@ __device__ __forceinline__ void jacobi_vcols(double* V, int64_t n, int p, int q,
   vq[k] = s * a + c * b;
 }
 
-// ||A||_F^2 -> *out (one workgroup)
-__global__ __launch_bounds__(256) void k_frob2(int64_t n, const double* __restrict__ A, int64_t lda, double* out) {
+// ||A||_F^2 in two fixed-order stages (deterministic): workgroup b sums the squares of columns
+// b, b + G, b + 2G, ... (G = gridDim.x) into part[b]; k_frob2_fin adds the G partial sums.
+__global__ __launch_bounds__(256) void k_frob2(int64_t n, const double* __restrict__ A, int64_t lda, double* part) {
   __shared__ double red[256];
   double acc = 0.0;
-  for (int64_t e = threadIdx.x; e < n * n; e += 256) {
-    const double v = A[(e / n) * lda + (e % n)];
-    acc = fma(v, v, acc);
-  }
+  for (int64_t j = blockIdx.x; j < n; j += gridDim.x)
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+      const double v = A[j * lda + i];
+      acc = fma(v, v, acc);
+    }
   red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(256) void k_frob2_fin(int np, const double* __restrict__ part, double* out) {
+  __shared__ double red[256];
+  red[threadIdx.x] = (int)threadIdx.x < np ? part[threadIdx.x] : 0.0;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
@@ -213,7 +225,10 @@ __device__ __forceinline__ int64_t bj_index(int P, int Q, int k) {
 }
 
 // per-pair scratch: G (BS x BS, column-major) | S' (BS x BS) ; rot flags (one int per pair)
-__global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const double* __restrict__ A, int64_t lda,
+// 1024 threads: one 2 x 2 block of S and two G pairs per thread per rotation round (the rounds
+// are latency-bound; 32 pairs per round of the circle ordering)
+constexpr int BJ_EIG_T = 1024;
+__global__ __launch_bounds__(BJ_EIG_T) void k_bj_eig(int n, int nbp, int r, const double* __restrict__ A, int64_t lda,
                                                 const double* frob2, double* __restrict__ gbuf,
                                                 int* __restrict__ rflag, int* __restrict__ nrot, int inner) {
   __shared__ double S[BS * BLD], G[BS * BLD];
@@ -225,7 +240,7 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
   circle_pair(nbp, r, pair, a, b);
   const int P = min(a, b), Q = max(a, b);
   // S from the lower triangle of A (symmetrised: the updates keep A symmetric only to rounding)
-  for (int e = tid; e < BS * BS; e += 256) {
+  for (int e = tid; e < BS * BS; e += BJ_EIG_T) {
     const int i = e % BS, j = e / BS;
     const int64_t gi = bj_index(P, Q, i), gj = bj_index(P, Q, j);
     double v = 0.0;
@@ -253,7 +268,7 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
       }
       __syncthreads();
       // S <- J^T S J, 2 x 2 blocks (row pair I, column pair K)
-      for (int e = tid; e < (BS / 2) * (BS / 2); e += 256) {
+      for (int e = tid; e < (BS / 2) * (BS / 2); e += BJ_EIG_T) {
         const int I = e % (BS / 2), K = e / (BS / 2);
         const double c1 = sc[I], s1 = ss[I], c2 = sc[K], s2 = ss[K];
         if (s1 == 0.0 && s2 == 0.0) continue;   // (s == 0 <=> identity: jacobi_rot's c is then 1)
@@ -270,7 +285,7 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
         S[q2 * BLD + q1] = z22;
       }
       // G <- G J (columns p, q of every row k)
-      for (int e = tid; e < (BS / 2) * BS; e += 256) {
+      for (int e = tid; e < (BS / 2) * BS; e += BJ_EIG_T) {
         const int I = e / BS, k = e % BS;
         const double c = sc[I], s = ss[I];
         if (s == 0.0) continue;
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(256) void k_bj_eig(int n, int nbp, int r, const dou
     if (nr == 0) break;
   }
   double* go = gbuf + (int64_t)pair * 2 * BS * BS;
-  for (int e = tid; e < BS * BS; e += 256) {
+  for (int e = tid; e < BS * BS; e += BJ_EIG_T) {
     const int i = e % BS, j = e / BS;
     go[e] = G[j * BLD + i];
     go[BS * BS + e] = S[j * BLD + i];
@@ -545,7 +560,12 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
   double* frob2 = ws + n;
   int* nrot = reinterpret_cast<int*>(ws + n + 8);
   double* V = ws + n + 64;
-  hipLaunchKernelGGL(k_frob2, dim3(1), dim3(256), 0, st, n, A, lda, frob2);
+  {
+    // partial sums in V's first G slots (G <= n <= n^2; k_eye overwrites them next)
+    const int G = (int)std::min<int64_t>(n, 256);
+    hipLaunchKernelGGL(k_frob2, dim3(G), dim3(256), 0, st, n, A, lda, V);
+    hipLaunchKernelGGL(k_frob2_fin, dim3(1), dim3(256), 0, st, G, V, frob2);
+  }
   hipLaunchKernelGGL(k_eye, dim3((unsigned)((n * n + 255) / 256)), dim3(256), 0, st, n, V);
   if (n <= JWG_MAX) {
     hipLaunchKernelGGL(k_jacobi_wg, dim3(1), dim3(1024), 0, st, (int)n, A, lda, V, frob2, info_dev);
@@ -557,7 +577,7 @@ int lstsq_sym_factor(void** rb, hipStream_t st, int64_t n, double* A, int64_t ld
     for (; sweep < JMAX_SWEEPS; ++sweep) {
       hipMemsetAsync(nrot, 0, sizeof(int), st);
       for (int r = 0; r < (int)nbp - 1; ++r) {
-        hipLaunchKernelGGL(k_bj_eig, dim3((unsigned)np), dim3(256), 0, st, (int)n, (int)nbp, r, A, lda, frob2, gbuf,
+        hipLaunchKernelGGL(k_bj_eig, dim3((unsigned)np), dim3(BJ_EIG_T), 0, st, (int)n, (int)nbp, r, A, lda, frob2, gbuf,
                            rflag, nrot, bj_inner_sweeps());
         if (bj_fused()) {
           // A in one tile pass, V's columns in the column kernel (z = 1 only)

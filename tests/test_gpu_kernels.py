@@ -278,8 +278,10 @@ def test_potrs_many_rhs_blocked(n, nrhs):
 
 def test_trsv_backward_solve_fails_loudly():
     """The persistent backward solve (k_trsv_bwd128) polls x_{B+1} with a bounded spin.  With the
-    bound shrunk to one sleep (debug knob), a consumer overtakes its producer: the device error
-    word must surface as IPMBackendError, never as a silently wrong step (VERDICT r2 #4)."""
+    bound shrunk to 1 us and chain ticket 1 storing its x block ~7 ms late (debug knobs), ticket 2's
+    poll runs out on every solve: the device error word must surface as IPMBackendError, never as a
+    silently wrong step.  (The bound alone is checked every 16 polls, so without
+    the late store a run may finish without tripping it.)"""
     from ipm355 import _lib as L
     h = handle()
     n = 8192
@@ -294,6 +296,7 @@ def test_trsv_backward_solve_fails_loudly():
     tripped = 0
     try:
         h.lib.ipm_debug_set_trsv_spin_limit(1)
+        h.lib.ipm_debug_set_trsv_publish_delay(-2 - 1)
         for _ in range(4):
             try:
                 potrs(Hm, n, n, b.copy())
@@ -301,8 +304,9 @@ def test_trsv_backward_solve_fails_loudly():
                 assert "spin bound" in str(e)
                 tripped += 1
     finally:
+        h.lib.ipm_debug_set_trsv_publish_delay(-1)
         h.lib.ipm_debug_set_trsv_spin_limit(0)
-    assert tripped >= 1
+    assert tripped == 4
     x = potrs(Hm, n, n, b.copy()).ravel()    # default bound again: correct, and no sticky error left
     np.testing.assert_allclose(x, ref, rtol=1e-10, atol=1e-12 * np.abs(ref).max())
 
