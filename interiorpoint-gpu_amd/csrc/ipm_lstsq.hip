@@ -250,7 +250,25 @@ __global__ __launch_bounds__(BJ_EIG_T) void k_bj_eig(int n, int nbp, int r, cons
   }
   const double tiny = DBL_EPSILON * sqrt(*frob2) / (double)n;
   int total = 0, sweep = 0;
+  if (tid == 0) srot = 0;
   __syncthreads();
+  // a subproblem none of whose 2016 pairs passes jacobi_rot's rotation test would come out of the
+  // sweep unchanged (G = I, S' = S, no rotation: S never changes, so every round sees the same
+  // entries) -- skip the 63 rounds then (most pairs of the last outer sweeps; bitwise the same)
+  {
+    int any = 0;
+    for (int e = tid; e < BS * BS; e += BJ_EIG_T) {
+      const int p = e % BS, q = e / BS;
+      if (p < q) {
+        const double ap = fabs(S[q * BLD + p]);
+        any |= (ap > DBL_EPSILON * sqrt(fabs(S[p * BLD + p]) * fabs(S[q * BLD + q])) && ap > tiny) ? 1 : 0;
+      }
+    }
+    if (any) srot = 1;   // (benign race: every writer stores 1)
+    __syncthreads();
+    if (srot == 0) inner = 0;
+    __syncthreads();
+  }
   for (; sweep < inner; ++sweep) {
     if (tid == 0) srot = 0;
     __syncthreads();
