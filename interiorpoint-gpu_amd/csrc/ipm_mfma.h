@@ -875,7 +875,13 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
                    ((((uintptr_t)a.Y) & 15) == 0);
   const int64_t ti128 = (a.ni + 127) / 128, tj128 = (a.nj + 127) / 128;
   const int64_t nblk128 = a.tri ? ti128 * (ti128 + 1) / 2 : ti128 * tj128;
-  const int BM = nblk128 >= 768 ? 128 : 64;
+  int BM = nblk128 >= 768 ? 128 : 64;
+  if (BM == 64 && ws) {
+    // a 128-tile grid just past whole rounds of the slots (SOCP n = 4096: 528 tiles on 512) takes
+    // the stream-K tail too, instead of the 64-tile grid's half-rate tiles
+    int64_t q0 = 0, K0 = 0;
+    if (streamk_plan(nblk128, slots, cap, a.K, q0, K0) > 0) BM = 128;
+  }
   const int64_t ti = (a.ni + BM - 1) / BM, tj = (a.nj + BM - 1) / BM;
   a.tiles_i = ti;
   a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
