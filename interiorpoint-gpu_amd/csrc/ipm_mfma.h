@@ -764,17 +764,20 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
 // stream-K plan for nt 128-tiles on `slots` slots: pieces per tile P (0: not worth it) and the
 // piece length Kp (whole 16-row slabs); the last piece of a tile may be shorter
 // IPM_STREAMK: 0 off (the K-halves split tail), 1 pieces first, 2 pieces last,
-// 3 pieces first with at most 8 pieces per tile (default: 2.37 -> 2.30 ms at n = 8192, K = 2048,
-// 2.63 -> 2.51 ms at n = 8100, K = 2050; profiles/r2_streamk_ab.txt)
-inline int streamk_mode() {
-  static const int mode = [] {
+// 3 pieces first with at most 8 pieces per tile (default from two rounds of tiles up: 2.37 -> 2.30
+// ms at n = 8192, K = 2048, 2.63 -> 2.51 ms at n = 8100, K = 2050; profiles/r2_streamk_ab.txt);
+// a grid of one round and a remainder defaults to 2 (SOCP n = 4096, 528 tiles on 512 slots:
+// 1.51 -> 1.46 ms, profiles/r4q)
+inline int streamk_mode(int64_t nt = 0, int slots = 0) {
+  static const int env = [] {
     const char* e = getenv("IPM_STREAMK");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : -1;
   }();
-  return mode;
+  if (env >= 0) return env;
+  return (slots > 0 && nt < 2 * (int64_t)slots) ? 2 : 3;
 }
 inline int streamk_plan(int64_t nt, int slots, int64_t cap, int64_t K, int64_t& q, int64_t& Kp) {
-  const int mode = streamk_mode();
+  const int mode = streamk_mode(nt, slots);
   q = 0;
   Kp = 0;
   if (!mode || slots <= 0 || nt < slots) return 0;
@@ -895,7 +898,7 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
       unsigned* cnt = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
       hipMemsetAsync(cnt, 0, (qk + npc) * sizeof(unsigned), st);
       dim3 g((unsigned)(npc + s_full)), blk(256);
-      const int pl = streamk_mode() == 2 ? 1 : 0;
+      const int pl = streamk_mode(a.nblk, slots) == 2 ? 1 : 0;
       if (a.w) {
         if (vec) hipLaunchKernelGGL((k_mfma_gemm_streamk<true, true>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
         else hipLaunchKernelGGL((k_mfma_gemm_streamk<true, false>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
