@@ -95,6 +95,8 @@ void ls_resid(hipStream_t st, const ResidView& v, double alpha0, double beta, un
 
 void border(hipStream_t st, int64_t n, double* H, int64_t ldh, const double* hxs, const double* hssp);
 void border_vec(hipStream_t st, int64_t n, const double* ct, const double* lbt, const double* ubt, double* out);
+// the same from the inverse bound slacks (squared inside: one launch instead of three)
+void border_vec_sq(hipStream_t st, int64_t n, const double* ct, const double* ilb, const double* iub, double* out);
 void t_minus(hipStream_t st, double t, const double* sp, double* out);
 
 }  // namespace ipm

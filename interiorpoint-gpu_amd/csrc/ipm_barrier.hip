@@ -669,6 +669,26 @@ __global__ void k_border_vec(int64_t n, const double* __restrict__ ct, const dou
 void border_vec(hipStream_t st, int64_t n, const double* ct, const double* lbt, const double* ubt, double* out) {
   if (n > 0) hipLaunchKernelGGL(k_border_vec, dim3(cdiv(n, 256)), dim3(256), 0, st, n, ct, lbt, ubt, out);
 }
+// the same with the bound terms squared in place (ilb[j]^2, iub[j]^2: each product rounded before
+// the sum, as the separate square kernels stored it) -- one launch instead of three
+__global__ void k_border_vec_sq(int64_t n, const double* __restrict__ ct, const double* __restrict__ ilb,
+                                const double* __restrict__ iub, double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  double v = ct ? -ct[j] : 0.0;
+  if (ilb) {
+    const double a = ilb[j], a2 = a * a;
+    v = v + a2;
+  }
+  if (iub) {
+    const double b = iub[j], b2 = b * b;
+    v = v - b2;
+  }
+  out[j] = v;
+}
+void border_vec_sq(hipStream_t st, int64_t n, const double* ct, const double* ilb, const double* iub, double* out) {
+  if (n > 0) hipLaunchKernelGGL(k_border_vec_sq, dim3(cdiv(n, 256)), dim3(256), 0, st, n, ct, ilb, iub, out);
+}
 
 // gs = t - sumv  (device scalar)
 __global__ void k_tminus(double t, const double* __restrict__ sp, double* __restrict__ out) {

@@ -2717,14 +2717,19 @@ struct TrinvSmem {
   double sDinv[8 * 256];
   double srinv[8 * 16];
 };
+// (y, ctl non-null: also resets the backward solve's state, saving two memset launches per solve:
+// y's block B to the pending pattern, and the solve's two control words by workgroup 0)
 __global__ __launch_bounds__(512, 1) void k_trinv128(int64_t n, const double* __restrict__ L, int64_t ldl,
-                                                     double* __restrict__ Xws) {
+                                                     double* __restrict__ Xws, double* __restrict__ y,
+                                                     unsigned* __restrict__ ctl) {
   __shared__ TrinvSmem sm;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int B = blockIdx.x;
   const int64_t r0 = (int64_t)B * TB2;
   const int rows = (int)min((int64_t)TB2, n - r0);
+  if (y && tid < rows) y[r0 + tid] = __longlong_as_double(-1LL);   // TRSV_PENDING
+  if (ctl && B == 0 && tid < 2) ctl[tid] = 0u;
   for (int idx = tid; idx < 36 * 256; idx += 512) {
     const int blk = idx >> 8, e = idx & 255, rr = e & 15, cc = e >> 4;
     int I = 0;
@@ -2975,17 +2980,17 @@ void set_trsv_publish_delay(int ticket) { g_trsv_delay_ticket.store(ticket); }
 void trsv_lower_t(hipStream_t st, int64_t n, const double* L, int64_t ldl, const double* b, int64_t bstride,
                   double* x, unsigned* ctl, double* xinv_ws, unsigned* err) {
   if (n <= 0) return;
-  hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned), st);
   // without the inverse workspace (or IPM_TRSV64=1): the 64-row substitution kernel
   static const bool k64 = [] { const char* e = getenv("IPM_TRSV64"); return e && e[0] == '1'; }();
   if (k64 || !xinv_ws || !err) {
+    hipMemsetAsync(ctl, 0, 2 * sizeof(unsigned), st);
     trsv_chain(st, false, n, L, ldl, b, bstride, x, ctl);
     return;
   }
   const int nblk = (int)cdiv(n, TB2);
-  hipLaunchKernelGGL(k_trinv128, dim3(nblk), dim3(512), 0, st, n, L, ldl, xinv_ws);
+  // (k_trinv128 also sets x to TRSV_PENDING in every row and zeroes ctl)
+  hipLaunchKernelGGL(k_trinv128, dim3(nblk), dim3(512), 0, st, n, L, ldl, xinv_ws, x, ctl);
   const int grid = std::min(nblk, 256);
-  hipMemsetAsync(x, 0xFF, n * sizeof(double), st);   // TRSV_PENDING in every row
   hipLaunchKernelGGL(k_trsv_bwd128, dim3(grid), dim3(512), 0, st, n, nblk, L, ldl, b, bstride, xinv_ws, x, ctl,
                      err,
                      g_trsv_delay_ticket.load(std::memory_order_relaxed));
@@ -3054,7 +3059,7 @@ void potrs_blocked(hipStream_t st, int64_t n, int64_t nrhs, const double* L, int
   double* XsT = Xs + nblk * 16384;
   double* Lp = XsT + nblk * 16384;   // Lp[k * n + c] = L(j0 + k, c), c < j0: block row j, transposed
   double* T = Lp + 128 * n;
-  hipLaunchKernelGGL(k_trinv128, dim3((unsigned)nblk), dim3(512), 0, st, n, L, ldl, Xs);
+  hipLaunchKernelGGL(k_trinv128, dim3((unsigned)nblk), dim3(512), 0, st, n, L, ldl, Xs, nullptr, nullptr);
   hipLaunchKernelGGL(k_block_transpose128, dim3((unsigned)cdiv(nblk * 16384, 256)), dim3(256), 0, st, nblk, Xs, XsT);
   auto gemm = [&](int64_t ni, int64_t nj, int64_t K, const double* X, int64_t ldx, const double* Y, int64_t ldy,
                   double* C, int64_t ldc, bool sub) {

@@ -404,11 +404,8 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool
       // border: hxs = -C^T inv_C^2 + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (+psd)
       if (pr->m > 0)
         gemv_t(st, pr->m, pr->n, 1.0, d.C, d.ldc, pr->inv, pr->inv, 0.0, pr->ct, pr->part, pr->part_elems);
-      const double* l2 = nullptr;
-      const double* u2 = nullptr;
-      if (d.lb) { square(st, pr->n, inv_lb(pr), pr->tmpn); l2 = pr->tmpn; }
-      if (d.ub) { square(st, pr->n, inv_ub(pr), pr->hxs); u2 = pr->hxs; }
-      border_vec(st, pr->n, pr->m > 0 ? pr->ct : nullptr, l2, u2, pr->hxs);
+      border_vec_sq(st, pr->n, pr->m > 0 ? pr->ct : nullptr, d.lb ? inv_lb(pr) : nullptr, d.ub ? inv_ub(pr) : nullptr,
+                    pr->hxs);
       ReduceBatch rb{};
       rb.ops[0] = ReduceOp{pr->inv, nullptr, pr->S, 1, 1, RED_SUMSQ, SC_SUMINV2};
       reduce(st, rb, 1, pr->scal);
@@ -427,11 +424,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool
       // hxs = -sum_i G_i inv_i + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (barrier segment)
       gemv_t(st, pr->K, pr->n, 1.0, d.X + (pr->R + pr->K) * d.ldx, d.ldx, pr->inv, nullptr, 0.0, pr->ct,
              pr->part, pr->part_elems);
-      const double* l2 = nullptr;
-      const double* u2 = nullptr;
-      if (d.lb) { square(st, pr->n, inv_lb(pr), pr->tmpn); l2 = pr->tmpn; }
-      if (d.ub) { square(st, pr->n, inv_ub(pr), pr->hxs); u2 = pr->hxs; }
-      border_vec(st, pr->n, pr->ct, l2, u2, pr->hxs);
+      border_vec_sq(st, pr->n, pr->ct, d.lb ? inv_lb(pr) : nullptr, d.ub ? inv_ub(pr) : nullptr, pr->hxs);
       ReduceBatch rb{};
       rb.ops[0] = ReduceOp{pr->inv, nullptr, pr->Sbar, 1, 1, RED_SUMSQ, SC_SUMINV2};
       reduce(st, rb, 1, pr->scal);
