@@ -1300,19 +1300,25 @@ struct RoleTrace {
   int ticket;
   unsigned long long t0;
   int role = -1;
+  // (NF fold tiles: wake = the spin's end, loaded = operands in registers; recorded instead of the
+  // ticket / CU key words)
+  unsigned long long wake = 0, loaded = 0;
   __device__ RoleTrace(bool o, int t) : on(o && t < 8192), ticket(t), t0(__builtin_amdgcn_s_memrealtime()) {}
   __device__ ~RoleTrace() {
     if (on && threadIdx.x == 0) {
-      ipm_role_trace[4 * ticket] = (unsigned long long)(unsigned)ticket | ((unsigned long long)(unsigned)role << 32);
+      const unsigned lo = wake ? (unsigned)(loaded - t0) : (unsigned)ticket;
+      ipm_role_trace[4 * ticket] = (unsigned long long)lo | ((unsigned long long)(unsigned)role << 32);
       ipm_role_trace[4 * ticket + 1] = t0;
       ipm_role_trace[4 * ticket + 2] = __builtin_amdgcn_s_memrealtime();
-      ipm_role_trace[4 * ticket + 3] = cu_key();
+      ipm_role_trace[4 * ticket + 3] = wake ? wake : cu_key();
     }
   }
 };
 #define ROLE(r) (rt.role = (r))
+#define ROLE_STAMP(f) (rt.f = __builtin_amdgcn_s_memrealtime())
 #else
 #define ROLE(r) ((void)0)
+#define ROLE_STAMP(f) ((void)0)
 #endif
 
 // FASTS: every trailing tile of this launch is a full 128-tile (K = 256): they run the
@@ -1545,18 +1551,50 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         return ld_ctl(&b.ctl[CTL_PA_NEXT]) >= (unsigned)nchd || ld_ctl(&b.ctl[CTL_PA_PROG]) == 0xFFFFFFFFu;
       });
     __syncthreads();
+    ROLE_STAMP(wake);
     const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, fk = lane >> 4;
     const int ib = 32 * ti + 16 * (wv & 1), jb = 32 * tj + 16 * (wv >> 1);
-    if (ib + 15 >= jb) {   // sub-tiles entirely above the diagonal are never read
-      const int i = ib + fr;
-      const bool iin = i < b.wbw;
-      dbl4 acc;
+    const bool live = ib + 15 >= jb;   // sub-tiles entirely above the diagonal are never read
+    const int i = ib + fr;
+    const bool iin = i < b.wbw, jin = jb + fr < b.wbw;
+    dbl4 acc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = jb + fk + 4 * r;
-        acc[r] = (iin && j < b.wbw) ? ld_sc1(&b.A[(k1 + j) * b.lda + k1 + i]) : 0.0;
+    for (int r = 0; r < 4; ++r) {
+      const int j = jb + fk + 4 * r;
+      acc[r] = (live && iin && j < b.wbw) ? ld_sc1(&b.A[(k1 + j) * b.lda + k1 + i]) : 0.0;
+    }
+    if constexpr (VEC) {
+      // the two 32-row blocks of L1D (rows 32 tj.. for the A operand, 32 ti.. for B; all 128
+      // columns) go to LDS with 16-byte direct loads: one wave instruction = 4 columns x 32 rows
+      // (lane l: rows 2 (l & 15), +1 of column l >> 4), element (c, r) of block s at
+      // sL[4096 s + 32 c + r].  16 instructions per wave instead of 64 8-byte strided loads, which
+      // ran past the 63 outstanding loads a wave may hold (r4u trace: 10.7 us from the wake to the
+      // operands, 2-3 us for the diagonal role's 128 KB panel the same way).  Rows past wbw read
+      // the next rows / column of the matrix (in bounds: P(b)'s columns follow) and are masked.
+      double* sL = sm.d.sD;
+      const int nsrc = ti == tj ? 1 : 2;
+      for (int it = wv; it < 32 * nsrc; it += 4) {
+        const int sblk = it >> 5, c4 = it & 31;
+        const int col = 4 * c4 + (lane >> 4);
+        const double* src = b.A + (b.cb + col) * b.lda + k1 + 32 * (sblk ? ti : tj) + 2 * (lane & 15);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)&sL[sblk * 4096 + c4 * 128], 16, 0,
+                                         16);   // aux 16 = sc1
       }
-      const bool jin = jb + fr < b.wbw;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      ROLE_STAMP(loaded);
+      if (live) {
+        const double* sa = sL + 16 * (wv >> 1) + fr;                          // L1D[jb + fr][k] at sa[32 k]
+        const double* sbp = sL + (ti == tj ? 0 : 4096) + 16 * (wv & 1) + fr;   // L1D[i][k]
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int k = 4 * q + fk;
+          const double av = jin ? -sa[32 * k] : 0.0, bv = iin ? sbp[32 * k] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+      }
+    } else if (live) {
       const double* pa = b.A + b.cb * b.lda + k1 + jb + fr;   // L1D[jb + fr][k] at pa[k * lda]
       const double* pbp = b.A + b.cb * b.lda + k1 + i;        // L1D[i][k]
       // all 64 operand loads in flight at once (one latency, not eight)
@@ -1569,12 +1607,12 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       }
 #pragma unroll
       for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);
-      if (iin) {
+    }
+    if (live && iin) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = jb + fk + 4 * r;
-          if (j < b.wbw) st_sc1(&b.A[(k1 + j) * b.lda + k1 + i], acc[r]);
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb + fk + 4 * r;
+        if (j < b.wbw) st_sc1(&b.A[(k1 + j) * b.lda + k1 + i], acc[r]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -40,3 +40,9 @@ for lo in range(0, int(st.max()) + 50, 50):
     m = (st >= lo) & (st < lo + 50)
     if m.any():
         print(f"    S tiles starting {lo:4d}-{lo + 50:4d} us: n={m.sum():4d} dur mean {du[m].mean():6.1f} min {du[m].min():6.1f}")
+# NF fold tiles (diagnostic build): spin end (wake), operands loaded, end -- us from the launch start
+s = a[(a[:, 0] >> 32) == 9]
+for row in s[np.argsort(s[:, 3])]:
+    wake, loaded = row[3], row[1] + (row[0] & 0xFFFFFFFF)
+    if 0 < wake - t0 < 10 ** 9:
+        print(f"    NF tile wake {(wake - t0) / 100:6.1f}  loaded {(loaded - t0) / 100:6.1f}  end {(row[2] - t0) / 100:6.1f}")
