@@ -207,50 +207,6 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
   a.dvec = e.dvec;
   a.info = info;
   a.tri = 1;
-  if (e.kend_dev && e.kend_host) {
-    a.kend256 = e.kend_dev;
-    // variable work per tile: contiguous tile runs per XCD of equal work (tri order)
-    const int BM = 128;
-    const int64_t T = cdiv(n, BM), nt = T * (T + 1) / 2;
-    if (nt >= 768) {
-      std::vector<double> wt(nt);
-      double tot = 0;
-      for (int64_t L = 0; L < nt; ++L) {
-        int64_t bi = (int64_t)((std::sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
-        while ((bi + 1) * (bi + 2) / 2 <= L) ++bi;
-        while (bi * (bi + 1) / 2 > L) --bi;
-        const int64_t bj = L - bi * (bi + 1) / 2, J = (bj * BM) >> 8;
-        const int64_t kt = std::min<int64_t>(k, J < e.nkend ? e.kend_host[J] : k);
-        wt[L] = (double)kt + 64.0;   // + epilogue (tP / H tile traffic) in k-row equivalents
-        tot += wt[L];
-      }
-      int64_t L = 0;
-      double acc = 0;
-      a.xb[0] = 0;
-      for (int x = 1; x < 8; ++x) {
-        while (L < nt && acc + 0.5 * wt[L] < tot * x / 8.0) acc += wt[L++];
-        a.xb[x] = (int)L;
-      }
-      a.xb[8] = (int)nt;
-      int maxc = 0;
-      for (int x = 0; x < 8; ++x) maxc = std::max(maxc, a.xb[x + 1] - a.xb[x]);
-      a.xbal = 1;
-      a.tiles_i = T;
-      a.nblk = nt;
-      const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
-                       ((((uintptr_t)a.Y) & 15) == 0);
-      dim3 g((unsigned)(8 * maxc)), b(256);
-      if (vec) hipLaunchKernelGGL((k_mfma_gemm<128, true, true>), g, b, 0, st, a);
-      else hipLaunchKernelGGL((k_mfma_gemm<128, true, false>), g, b, 0, st, a);
-      return;
-    }
-  }
-  // super-block tile order (tri_sb_index; IPM_SYRK_SB = block size in tiles, 0 = row order)
-  static const int sb = [] { const char* v = getenv("IPM_SYRK_SB"); return v ? atoi(v) : 0; }();
-  if (sb > 0) {
-    a.sb = sb;
-    a.xcd_remap = 0;   // (tri_sb_index applies the XCD-contiguous runs itself)
-  }
   if (e.split_ws) mfma_gemm_launch_split(st, a, e.split_ws, e.split_cap, 2 * num_cus());
   else mfma_gemm_launch(st, a);
 }
@@ -969,9 +925,7 @@ enum {
   // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
   // by a workgroup that landed on that CU
   CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
-  CTL_XQ = CTL_SPILL + NCRIT,         // trailing-tile queue counter of each XCD (8 words)
-  CTL_FLEX_S = CTL_XQ + 8, CTL_FLEX_R,  // flexible tickets: trailing tiles / row chunks taken
-  CTL_HDR = CTL_FLEX_R + 1
+  CTL_HDR = CTL_SPILL + NCRIT
 };
 
 // Row role: rows below the diagonal block, L21 = A21 L11^-T, 64 rows per workgroup, 16 rows per
@@ -1132,47 +1086,6 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
   }
 }
 
-// One panel (width nb <= 128 at column k0) in ONE launch.  Workgroups draw tickets: ticket 0 is the
-// diagonal role (so it is resident before anyone waits on it -- no deadlock for any residency),
-// tickets 1.. are the row chunks, pipelined one block column behind the diagonal role.
-// next_nb > 0 (nb == 128): the row chunks also apply this panel to the next panel's columns.
-// ctl: 4 zeroed words {ticket, progress, next-diagonal rows published, -}.
-__global__ __launch_bounds__(256, 2) void k_potrf_panel(int64_t n, int64_t k0, int nb, int next_nb,
-                                                     double* __restrict__ A, int64_t lda, double* ws, unsigned* ctl,
-                                                     int* __restrict__ info) {
-  __shared__ DiagSmem sm;
-  __shared__ int sticket, sflag;
-  if (threadIdx.x == 0) sticket = (int)atomicAdd(&ctl[0], 1u);
-  __syncthreads();
-  const int t = sticket;
-  double* dinv = ws;
-  double* pubL = ws + PF_DINV;
-  if (t == 0) {
-    diag_role(k0, nb, A, lda, dinv, info, pubL, &ctl[1], sm);
-  } else {
-    if (*info != 0) return;
-    row_role(t - 1, n, k0, nb, A, lda, dinv, pubL, &ctl[1], next_nb, &ctl[2], sm.sD, &sflag);
-  }
-}
-
-// one panel of width nb <= 128 at column k0 (ctl: this panel's 4 zeroed control words);
-// next_nb > 0 requires nb == 128 and k0 + nb + next_nb <= n
-static void panel_launch(hipStream_t st, int64_t n, int64_t k0, int nb, double* A, int64_t lda, int* info,
-                         double* ws, unsigned* ctl, int next_nb = 0) {
-  const int64_t below = n - k0 - nb;
-  hipLaunchKernelGGL(k_potrf_panel, dim3(1 + cdiv(std::max<int64_t>(below, 0), PF_RB)), dim3(256), 0, st, n, k0,
-                     nb, next_nb, A, lda, ws, ctl, info);
-}
-// fused intra-block update in the first panel of a block (IPM_NO_FOLD=1: separate GEMM launch)
-static bool fold_intra() {
-  static int f = -1;
-  if (f < 0) {
-    const char* e = getenv("IPM_NO_FOLD");
-    f = (e && atoi(e) == 1) ? 0 : 1;
-  }
-  return f == 1;
-}
-
 // =====================================================================================
 // One launch per 256-column block (default path).  Block b = columns [cb, cb + wa + wbw):
 //   LA  tiles : A[cb:n, block b] -= L[cb:n, block b-1] L[block b, block b-1]^T   (64-tiles,
@@ -1200,21 +1113,8 @@ struct BlockArgs {
   int nla = 0, nra = 0, nrb = 0, la_tj = 0, nlab = 0;
   int64_t ns = 0;
   int nnf = 0;                  // next-diagonal-block fold tiles (32 x 32, lower triangle)
-  int s_map = 0;                // trailing-tile order (IPM_S_MAP)
-  // deferred KKT-SYRK slices run by this launch (DeferSyrk): job q = block column gs_J[q], slice
-  // gs_s[q] (first: G written, else accumulated), 64-tiles gs_cum[q] .. gs_cum[q+1]
-  static constexpr int MAXGS = 12;
-  int ngs = 0;
-  int gs_J[MAXGS] = {}, gs_s[MAXGS] = {}, gs_first[MAXGS] = {};
-  int64_t gs_cum[MAXGS + 1] = {};
-  int64_t gs_total = 0;          // == gs_cum[ngs]
-  const double* gX = nullptr;
-  const double* gw = nullptr;
-  double* G = nullptr;
-  int64_t gldx = 0, ldg = 0, gns = 0, gm = 0;
-  int gKS = 0;
   GemmArgs la32, la, la128, s;   // look-ahead: 32-tiles (rows, cols < 128, lower), 64-tiles (rows
-                                 // 128..255, or all rows >= 128 when deferring), 128-tiles (rows >= 256)
+                                 // 128..255, or all rows >= 128 below IPM_LA128_MIN), 128-tiles (rows >= 256)
   int nla32 = 0, la32_T = 0, nla64 = 0, nla128 = 0;
   int trace = 0;                // IPM_ROLE_TRACE builds: record this launch's roles
   // ragged trailing rows (IPM_RAG, default on): the last rag_n <= 8 rows of the trailing update,
@@ -1236,36 +1136,7 @@ struct BlockArgs {
   GemmArgs s2;
   int rag_K = CH_NB;            // ragged rows: K extent and first column of the applied blocks
   int64_t rag_cp = 0;
-  int flex = 0;                 // IPM_FLEX: trailing tiles and non-critical row chunks share tickets
-  // trailing tiles around the non-critical row chunks (row_slots): S tickets [0, sa), the other
-  // P(a) row chunks, S [sa, sb), the P(b) row chunks, S [sb, ns).  sa = sb = ns: rows last.
-  // rpad_a / rpad_b: no-op tickets after each row group placed among the S tiles, so that the
-  // S tickets keep their ticket-mod-8 XCD phase (the XCD-contiguous tile runs, xcd_remap)
-  int64_t sa = 0, sb = 0;
-  int rpad_a = 0, rpad_b = 0;
-  int rowprio = 0;              // s_setprio of the non-critical row chunks (IPM_ROWPRIO)
 };
-#ifndef FLEX_PROG
-#define FLEX_PROG 4   // block rows of its diagonal role published before a row chunk is taken early
-#endif
-
-// Trailing tiles by XCD (s_map 2): the tri tile list is cut into 8 contiguous runs; a workgroup
-// takes the next tile of ITS XCD's run (HW_REG_XCC_ID); an exhausted run sends it on to the next
-// XCD's run.  One pass over the 8 runs always finds a tile (each tile-ticket takes exactly one
-// and runs are never refilled).  Returns the tile index in the tri enumeration.
-__device__ __forceinline__ int64_t xcd_tile(unsigned* xq, int64_t ntiles) {
-  const int64_t q = ntiles >> 3, rem = ntiles & 7;
-  const unsigned x0 = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // HW_REG_XCC_ID
-  for (unsigned d = 0; d < 8; ++d) {
-    const unsigned x = (x0 + d) & 7u;
-    const int64_t len = q + ((int64_t)x < rem ? 1 : 0), start = (int64_t)x * q + std::min<int64_t>(x, rem);
-    if ((int64_t)ld_ctl(&xq[x]) >= len) continue;
-    const int64_t i = (int64_t)atomicAdd(&xq[x], 1u);
-    if (i < len) return start + i;
-  }
-  return -1;   // unreachable (see above)
-}
-
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
 __device__ __forceinline__ unsigned cu_key() {
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -1327,7 +1198,8 @@ struct RoleTrace {
 // K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
 // before the first MFMA
 template <bool VEC, bool FASTS = false, int LAZY = 0>
-__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
+__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
+  IPM_KARGS(BlockArgs, b, b_arg);   // (fields loaded where each role uses them: ipm_mfma.h)
   __shared__ BlockSmem sm;
   __shared__ int sticket, sflag;
   const int tid = threadIdx.x;
@@ -1356,16 +1228,14 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     ROLE(0);
     int64_t rb;
     if (t < b.nla32) {
-      if (b.la32.C2) mfma_tile<32, false, VEC, 2, true, true>(b.la32, t, sm.g32);
-      else mfma_tile<32, false, VEC, 2, true>(b.la32, t, sm.g32);
+      mfma_tile<32, false, VEC, 2, true>(b.la32, t, sm.g32);
       int64_t i = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);   // tri row of tile t
       while ((i + 1) * (i + 2) / 2 <= t) ++i;
       while (i * (i + 1) / 2 > t) --i;
       rb = i >> 1;
     } else if (t - b.nla32 < b.nla64) {
       const int64_t t64 = t - b.nla32;
-      if (b.la.C2) mfma_tile<64, false, VEC, 2, true, true>(b.la, t64, sm.g64);
-      else mfma_tile<64, false, VEC, 2, true>(b.la, t64, sm.g64);
+      mfma_tile<64, false, VEC, 2, true>(b.la, t64, sm.g64);
       rb = 2 + t64 / b.la_tj;
     } else {
       // rows >= 256: 128-tiles (only the later P(a) row chunks wait for them); two 64-row blocks
@@ -1402,12 +1272,13 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   };
   const int64_t k1 = b.cb + b.wa;
   // ticket order after the LA tiles: P(a) diagonal, the P(a) row chunks holding P(b)'s diagonal
-  // block rows (nchd), the tiles folding P(a) into that block (NF), P(b) diagonal, S tiles, the
-  // other P(a) row chunks, P(b) row chunks.  Row chunks spin while their diagonal role works;
-  // dispatched after the S tiles they do not hold slots the trailing update could use.  Decode first, then ONE call site per role (each role's code
-  // is inlined once: register pressure and code size).
+  // block rows (nchd), the tiles folding P(a) into that block (NF), P(b) diagonal, ragged-row
+  // workgroups, S tiles, the other P(a) row chunks, P(b) row chunks.  Row chunks spin while their
+  // diagonal role works; dispatched after the S tiles they do not hold slots the trailing update
+  // could use.  Decode first, then ONE call site per role (each role's code is inlined once:
+  // register pressure and code size).
   const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_GS, K_RAG, K_NONE } kind = K_NONE;
+  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_RAG, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
   if (t == 0) {
@@ -1427,68 +1298,15 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
       const int64_t na = b.nra - nchd;
       if (t < b.nrag) {
         kind = K_RAG;
-      } else if (b.flex && (t -= b.nrag) < b.ns + na + b.nrb) {
-        // flexible tickets: one item each from two queues -- the remaining row chunks (P(a) ones,
-        // then P(b) ones) once their diagonal role has published FLEX_PROG block rows, else the
-        // next trailing tile.  Every ticket gets exactly one item (tickets = items; a ticket finding
-        // the tile queue exhausted takes a row chunk regardless).  A row chunk then waits only for
-        // its diagonal role, look-ahead tiles (lower tickets) and, for P(b), P(a) chunks that an
-        // earlier flexible ticket took: no cycle.  Row chunks start as their panel is ready instead
-        // of after every trailing tile.
-        __shared__ long long sflex;
-        if (tid == 0) {
-          const unsigned nr = (unsigned)(na + b.nrb), nsv = (unsigned)b.ns;
-          long long item = -1;
-          const unsigned r = ld_ctl(&b.ctl[CTL_FLEX_R]);
-          const bool ready = r < nr && ld_ctl(&b.ctl[r < (unsigned)na ? CTL_PA_PROG : CTL_PB_PROG]) >= (unsigned)FLEX_PROG;
-          if (ready) {
-            const unsigned r2 = atomicAdd(&b.ctl[CTL_FLEX_R], 1u);
-            if (r2 < nr) item = (1ll << 40) | r2;
-          }
-          if (item < 0) {
-            const unsigned s2 = atomicAdd(&b.ctl[CTL_FLEX_S], 1u);
-            if (s2 < nsv) item = s2;
-          }
-          if (item < 0) {
-            const unsigned r2 = atomicAdd(&b.ctl[CTL_FLEX_R], 1u);
-            if (r2 < nr) item = (1ll << 40) | r2;
-          }
-          sflex = item;
-        }
-        __syncthreads();
-        const long long it = sflex;
-        if (it >= (1ll << 40)) {
-          const int64_t r = it & 0xFFFFFFFFll;
-          kind = K_ROW;
-          pb = r >= na;
-          chunk = pb ? r - na : nchd + r;
-        } else if (it >= 0) {
-          kind = K_TILE;
-          t = it;
-        }
-      } else if (b.flex) {
-        if ((t -= b.ns + na + b.nrb) < b.gs_total) kind = K_GS;
-      } else if ((t -= b.nrag) < b.sa) {
+      } else if ((t -= b.nrag) < b.ns) {
         kind = K_TILE;
-      } else if ((t -= b.sa) < na + b.rpad_a) {
-        if (t < na) {   // (else a padding ticket: nothing)
-          kind = K_ROW;
-          chunk = nchd + t;
-        }
-      } else if ((t -= na + b.rpad_a) < b.sb - b.sa) {
-        kind = K_TILE;
-        t += b.sa;
-      } else if ((t -= b.sb - b.sa) < b.nrb + b.rpad_b) {
-        if (t < b.nrb) {
-          kind = K_ROW;
-          pb = true;
-          chunk = t;
-        }
-      } else if ((t -= b.nrb + b.rpad_b) < b.ns - b.sb) {
-        kind = K_TILE;
-        t += b.sb;
-      } else if ((t -= b.ns - b.sb) < b.gs_total) {
-        kind = K_GS;   // last: they fill the CUs the chain leaves idle
+      } else if ((t -= b.ns) < na) {
+        kind = K_ROW;
+        chunk = nchd + t;
+      } else if ((t -= na) < b.nrb) {
+        kind = K_ROW;
+        pb = true;
+        chunk = t;
       }
     }
   }
@@ -1521,10 +1339,6 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
   }
   if (kind == K_ROW) {
     ROLE(pb ? 6 : (chunk < nchd ? 2 : 5));
-    // (latency-bound MFMA chains: beside trailing tiles they win the issue arbitration)
-    if (b.rowprio == 1) __builtin_amdgcn_s_setprio(1);
-    else if (b.rowprio == 2) __builtin_amdgcn_s_setprio(2);
-    else if (b.rowprio >= 3) __builtin_amdgcn_s_setprio(3);
     if (pb) {
       // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
       const int64_t r0 = b.wbw + chunk * PF_RB;
@@ -1620,50 +1434,6 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     if (tid == 0) __hip_atomic_fetch_add(&b.ctl[CTL_NF], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  if (kind == K_GS) {
-    ROLE(10);
-    // never beside a critical-path role: wait (holding the slot) until none runs on this CU
-    if (tid == 0) {
-      const unsigned me = 1u + cu_key();
-      spin_until<20>(b.info, failw, [&] {
-        bool busy = false;
-        for (int i = 0; i < NCRIT; ++i) busy |= ld_ctl(&b.ctl[CTL_CRIT + i]) == me;
-        return !busy;
-      });
-    }
-    __syncthreads();
-    // G(:, block J) (+)= C_s^T diag(w_s) C_s over this job's k rows (64 x 64 tiles, rows >= 256 J)
-    // job lookup with constant indices only (a dynamically indexed kernel-argument array would
-    // put the whole argument block in scratch memory)
-    int gJ = 0, gsl = 0, gfirst = 0;
-    int64_t gbase = 0;
-#pragma unroll
-    for (int i = 0; i < BlockArgs::MAXGS; ++i)
-      if (i < b.ngs && t >= b.gs_cum[i]) {
-        gJ = b.gs_J[i];
-        gsl = b.gs_s[i];
-        gfirst = b.gs_first[i];
-        gbase = b.gs_cum[i];
-      }
-    const int64_t J0 = (int64_t)gJ * CH_NB, k0 = (int64_t)gsl * b.gKS;
-    GemmArgs g;
-    g.ni = b.gns - J0;
-    g.nj = std::min<int64_t>(CH_NB, b.gns - J0);
-    g.K = std::min<int64_t>(b.gKS, b.gm - k0);
-    g.X = g.Y = b.gX + k0 * b.gldx + J0;
-    g.ldx = g.ldy = b.gldx;
-    g.w = b.gw + k0;
-    g.C = b.G + J0 * b.ldg + J0;
-    g.ldc = b.ldg;
-    g.accum = gfirst ? 0 : 1;
-    g.rowmajor = 1;
-    g.xcd_remap = 0;
-    g.tiles_j = (g.nj + 63) / 64;
-    g.tiles_i = (g.ni + 63) / 64;
-    g.nblk = g.tiles_i * g.tiles_j;
-    mfma_tile<64, true, true, 2, false>(g, t - gbase, sm.g64);
-    return;
-  }
   if (kind == K_RAG) {
     ROLE(12);
     // ragged rows i in [r0, r0 + rn) of the trailing update (origin o, K = the previous block's
@@ -1705,7 +1475,6 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
     // the chain.  Every tile workgroup, after its own tile, takes what is in the spill words; the
     // sleeper, once the role is done, runs its tile itself if nobody took it.
     if (tid == 0) {
-      if (b.s_map == 2) t = xcd_tile(&b.ctl[CTL_XQ], b.ns);   // this workgroup's tile: its XCD's run
       const unsigned me = 1u + cu_key();
       int q = -1;
       for (int i = 0; i < NCRIT && q < 0; ++i)
@@ -1752,7 +1521,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b) {
         }
         // (both loops in one kernel raised the SGPR spills 89 -> 621 and cost 2.5 %: the launch
         // picks the kernel instead, FASTS)
-        mfma_tile<128, false, VEC, 2, false, false, false, (FASTS && VEC) ? 1 : 0, (FASTS && VEC) ? LAZY : 0>(
+        mfma_tile<128, false, VEC, 2, false, false, (FASTS && VEC) ? 1 : 0, (FASTS && VEC) ? LAZY : 0>(
             g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
                      : b.f0 + (u < 0 ? st : b.s_full + p),
             sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p, -1, -1, b.info, failw);
@@ -1825,51 +1594,6 @@ static std::vector<std::pair<int64_t, double>> launch_items(int64_t nla, int64_t
   span(sb, e2);
   return it;
 }
-// ---- where the non-critical row chunks go among the trailing tiles (IPM_ROWPOS=1).  The rest of
-// P(a)'s row chunks can run once its diagonal role is done (~0.7 tile units into a launch), P(b)'s
-// once its own is (~1.3, role timelines in DESIGN.md).  Queued behind every trailing tile they all
-// start in the last round and hold the launch open after the tiles drain (block 4 of n = 8192:
-// the last 85 of 415 us); here each goes before the first S ticket the list schedule dispatches
-// after its panel is ready.  sa = sb = ns_all keeps them last.
-static void row_slots(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t nstrip, int64_t ns_all,
-                      double tc, double lac, int64_t nra, double ta, double tb, int64_t& sa, int64_t& sb) {
-  sa = sb = ns_all;
-  if (ns_all < 64) return;
-  const int slots = 2 * num_cus();
-  std::priority_queue<double, std::vector<double>, std::greater<double>> h;
-  for (int i = 0; i < slots; ++i) h.push(0.0);
-  auto run = [&](int64_t cnt, double d) {
-    for (int64_t k = 0; k < cnt; ++k) {
-      const double t0 = h.top();
-      h.pop();
-      h.push(t0 + d);
-    }
-  };
-  run(nla, lac);
-  run(1, 0.6);
-  run(nchd, 0.66);
-  run(nnf, 0.8);
-  run(pb ? 1 : 0, 1.25);
-  run(nrag, 0.1 * tc);
-  bool placed_a = false;
-  int64_t i = 0;
-  while (i < ns_all) {
-    const double t0 = h.top();
-    if (!placed_a && t0 >= ta) {
-      sa = i;
-      placed_a = true;
-      run(nra, 0.5);
-      continue;   // (the rows took slots: re-read the next dispatch time)
-    }
-    if (placed_a && t0 >= tb) {
-      sb = i;
-      return;
-    }
-    h.pop();
-    h.push(t0 + tc);
-    ++i;
-  }
-}
 static int64_t plan_split(int64_t nla, int64_t nchd, int64_t nnf, bool pb, int64_t nrag, int64_t ns, int64_t nrows,
                           int64_t cap, double tc = 1.0, int64_t nstrip = 0, double lac = 0.8, int64_t nra = -1,
                           int64_t sa = -1, int64_t sb = -1) {
@@ -1905,7 +1629,7 @@ struct PairPlan {
   std::vector<int> kind;      // per 256-column block
   std::vector<int64_t> f1;    // EVEN: F tiles it takes (tile list [0, f1)); ODD: the EVEN's f1
 };
-static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks, bool defer) {
+static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks) {
   PairPlan pl;
   pl.kind.assign(nblocks, 0);
   pl.f1.assign(nblocks, 0);
@@ -1915,7 +1639,7 @@ static PairPlan potrf_pair_plan(int64_t n, int64_t ncols, int64_t nblocks, bool 
   // 6.40 -> 6.22 ms (6656: 6.31, 5632: 6.35; profiles/r3_pair_sweep.txt).  IPM_PAIR=0: off.
   static const bool on = [] { const char* e = getenv("IPM_PAIR"); return !(e && e[0] == '0'); }();
   static const int64_t minrows = [] { const char* e = getenv("IPM_PAIR_MIN"); return e ? atoll(e) : 6144LL; }();
-  if (!on || defer || ncols < n - 8) return pl;   // (a partial factorisation keeps the plain order)
+  if (!on || ncols < n - 8) return pl;   // (a partial factorisation keeps the plain order)
   // EVEN e needs block e+1 to exist and F = rows beyond block e+1 of at least minrows
   int64_t last = -1;
   for (int64_t e = 2; e + 1 < nblocks; e += 2) {
@@ -1951,9 +1675,7 @@ static void set_spin_ticks(int which, unsigned us) {
 }
 void set_potrf_spin_limit_us(unsigned us) { set_spin_ticks(0, us); }
 
-void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
-                       const DeferSyrk* ds) {
-  const bool defer = ds && ds->active();
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
   if (ncols < 0 || ncols > n) ncols = n;
   if (ncols <= 0) {
     hipMemsetAsync(info, 0, sizeof(int), st);
@@ -1974,7 +1696,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   const char* elz = getenv("IPM_LAZYC");
   const bool lazy_on = !(elz && elz[0] == '0');
   const bool lazy2_on = lazy_on && !(elz && elz[0] == '1');   // IPM_LAZYC=1: K = 256 tiles only
-  PairPlan pl = potrf_pair_plan(n, ncols, nblocks, defer);
+  PairPlan pl = potrf_pair_plan(n, ncols, nblocks);
   for (int64_t bk = 0; bk < nblocks; ++bk) {
     const int kind = pl.kind[bk];
     const int64_t Kla = kind == 2 ? 2 * CH_NB : CH_NB;   // look-ahead depth (EVEN: the pair)
@@ -2012,13 +1734,13 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       b.nla32 = (int)c.nblk;
       b.la32_T = (int)c.tiles_i;
       // rows [128, 256) x all wb columns: 64-tiles, row blocks in order (P(b)'s diagonal rows: on
-      // the chain); rows >= 256: 128-tiles (IPM_LA128=0: 64-tiles throughout, as when deferring)
+      // the chain); rows >= 256: 128-tiles (IPM_LA128=0: 64-tiles throughout)
       static const bool la128_on = [] { const char* e = getenv("IPM_LA128"); return !e || e[0] != '0'; }();
       // 128-tiles only while more than la128_min rows remain below cb: with fewer, the 64-tiles'
       // shorter tiles reach the P(a) row chunks sooner (profiles/r4m: n = 2048 0.864 -> 0.814 ms,
       // 4096 1.97 -> 1.87, 8193 6.23 -> 6.16; IPM_LA128_MIN=<rows>, 0 = always 128-tiles)
       static const int64_t la128_min = [] { const char* e = getenv("IPM_LA128_MIN"); return e ? atoll(e) : 3072LL; }();
-      const bool use128 = la128_on && ni > la128_min && !(defer && bk < ds->nblocks && ds->d[bk] > 0);
+      const bool use128 = la128_on && ni > la128_min;
       GemmArgs& a = b.la;
       a.ni = std::max<int64_t>((use128 ? std::min<int64_t>(ni, 256) : ni) - 128, 0);
       a.nj = wb;
@@ -2049,16 +1771,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       b.nla = b.nla32 + b.nla64 + b.nla128;
       b.la_tj = (int)a.tiles_j;
       b.nlab = (int)cdiv(ni, 64);
-      if (defer && bk < ds->nblocks && ds->d[bk] > 0 && cb < ds->ns) {
-        // block column bk's deferred KKT slices (G) join its look-ahead update
-        c.C2 = ds->G + cb * ds->ldg + cb;
-        c.ldc2 = ds->ldg;
-        c.n2 = c.n2c = ds->ns - cb;
-        a.C2 = ds->G + cb * ds->ldg + cb + 128;
-        a.ldc2 = ds->ldg;
-        a.n2 = ds->ns - cb - 128;
-        a.n2c = ds->ns - cb;
-      }
       const int64_t m = n - cb - wb;
       b.rag_cp = cb - CH_NB;
       b.rag_K = CH_NB;
@@ -2147,11 +1859,7 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
         g.ldc = lda;
         g.sub = 1;
         g.tri = 1;
-        // trailing-tile order (IPM_S_MAP): 0 = XCD-remapped ticket order, 1 = plain tri order,
-        // 2 = per-XCD runs by HW_REG_XCC_ID
-        static const int smap = [] { const char* e = getenv("IPM_S_MAP"); return e ? atoi(e) : 0; }();
-        b.s_map = smap;
-        g.xcd_remap = smap == 0 ? 1 : 0;
+        g.xcd_remap = 1;   // XCD-contiguous tile runs
         g.tiles_i = cdiv(ms, 128);
         g.nblk = g.tiles_i * (g.tiles_i + 1) / 2;
         b.ns = g.nblk;
@@ -2170,10 +1878,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       const int T = (int)cdiv(b.wbw, 32);
       b.nnf = T * (T + 1) / 2;
     }
-    static const bool flex_on = [] { const char* e = getenv("IPM_FLEX"); return e && e[0] == '1'; }();
-    // IPM_ROWPOS=1: the non-critical row chunks among the trailing tiles (row_slots)
-    static const bool rowpos_on = [] { const char* e = getenv("IPM_ROWPOS"); return e && e[0] == '1'; }();
-    b.sa = b.sb = b.ns;
     // a plain launch whose trailing tiles can all run the lazy-C loop keeps them whole: the lazy
     // kernel gains more than the K-halves of the last round (r3: 6.20 -> 6.12-6.16 ms at n = 8192)
     static const bool fasts_on = [] { const char* e = getenv("IPM_FASTS"); return !(e && e[0] == '0'); }();
@@ -2181,85 +1885,34 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     const bool lazy_cand = lazy_on && fasts_on && vec && (b.s.ni % 128) == 0 &&
                            ((b.s.K == CH_NB && b.nstrip == 0) || (lazy2_on && b.s.K == 2 * CH_NB));
     const bool split_here = split_on && !lazy_cand;
-    if (b.s_full > 0 && !defer && (split_here || rowpos_on)) {
-      // the planner's split count and row positions (cached per size and block: they depend on
-      // nothing else)
-      struct Plan { int64_t q = -1, sa = 0, sb = 0; };
+    if (b.s_full > 0 && split_here) {
+      // the planner's split count (cached per size and block: it depends on nothing else)
       static std::mutex mu;
-      static std::map<std::tuple<int64_t, int64_t, int>, std::vector<Plan>> cache;
+      static std::map<std::tuple<int64_t, int64_t, int>, std::vector<int64_t>> cache;
       const int nchd_h = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
       const double tc = b.s.K > CH_NB ? 1.6 : 1.0, lac = Kla > CH_NB ? 1.6 : 0.8;
       const int64_t nra_h = b.nra - nchd_h;
-      Plan p;
+      int64_t q = 0;
       {
         std::lock_guard<std::mutex> lk(mu);
-        // (split_here in the key: with IPM_ROWPOS=1 a launch that may not split must never reuse a
-        // plan with q > 0 -- its split scratch and flags are not set up)
-        auto& v = cache[{n, ncols, (split_here ? 1 : 0) | (rowpos_on && !flex_on ? 2 : 0) | (lazy_on ? 4 : 0) |
-                                       (lazy2_on ? 8 : 0) | (vec ? 16 : 0)}];
-        if ((int64_t)v.size() < nblocks) v.assign(nblocks, Plan{});
-        if (v[bk].q < 0) {
-          Plan& w = v[bk];
-          w.sa = w.sb = b.ns;
-          if (rowpos_on && !flex_on) {
-            static const double ta = [] { const char* e = getenv("IPM_ROW_TA"); return e ? atof(e) : 0.75; }();
-            static const double tb = [] { const char* e = getenv("IPM_ROW_TB"); return e ? atof(e) : 1.35; }();
-            row_slots(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.nstrip, b.ns, tc, lac, nra_h, ta, tb, w.sa, w.sb);
-          }
-          w.q = split_here ? plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, nra_h + b.nrb,
-                                      potrf_split_cap(n), tc, b.nstrip, lac, nra_h, w.sa, w.sb)
-                         : 0;
+        auto& v = cache[{n, ncols, (lazy_on ? 4 : 0) | (lazy2_on ? 8 : 0) | (vec ? 16 : 0)}];
+        if ((int64_t)v.size() < nblocks) v.assign(nblocks, -1);
+        if (v[bk] < 0) {
+          v[bk] = plan_split(b.nla, nchd_h, b.nnf, b.wbw > 0, b.nrag, b.s_full, nra_h + b.nrb, potrf_split_cap(n),
+                             tc, b.nstrip, lac);
           static const bool dbg = getenv("IPM_SPLIT_DEBUG") != nullptr;
           if (dbg)
-            fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld, rows before S %ld / %ld\n",
-                    (long)n, (long)bk, (long)b.ns, (long)w.q, (long)w.sa, (long)w.sb);
+            fprintf(stderr, "potrf n=%ld block %ld: %ld trailing tiles, split %ld\n", (long)n, (long)bk, (long)b.ns,
+                    (long)v[bk]);
         }
-        p = v[bk];
+        q = v[bk];
       }
-      if (!split_here) p.q = 0;
-      b.s_full -= p.q;
-      b.ns = b.nstrip + b.s_full + 2 * p.q;
-      b.sa = std::min(p.sa, b.ns);
-      b.sb = std::min(std::max(p.sb, b.sa), b.ns);
-      static const bool rpad_on = [] { const char* e = getenv("IPM_ROWPAD"); return !(e && e[0] == '0'); }();
-      if (rpad_on && b.sa < b.ns) b.rpad_a = (8 - (b.nra - nchd_h) % 8) % 8;
-      if (rpad_on && b.sb < b.ns) b.rpad_b = (8 - b.nrb % 8) % 8;
-      if (split_here) {
-        b.sscr = ws + potrf_split_scratch_off(n);
-        b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
-      }
+      b.s_full -= q;
+      b.ns = b.nstrip + b.s_full + 2 * q;
+      b.sscr = ws + potrf_split_scratch_off(n);
+      b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
     }
-    static const int rowprio = [] { const char* e = getenv("IPM_ROWPRIO"); return e ? atoi(e) : 0; }();
-    b.rowprio = rowprio;
-    if (defer) {
-      // slices of the blocks J ahead whose deferral window [J - d[J], J) holds this launch
-      b.gX = ds->X;
-      b.gldx = ds->ldx;
-      b.gw = ds->w;
-      b.G = ds->G;
-      b.ldg = ds->ldg;
-      b.gns = ds->ns;
-      b.gm = ds->m;
-      b.gKS = ds->KS;
-      for (int J = (int)bk + 1; J < ds->nblocks && J - 1 - bk < 64 && b.ngs < BlockArgs::MAXGS; ++J) {
-        const int dJ = ds->d[J];
-        const int off = J - 1 - (int)bk;             // bit of this launch in lm[J]
-        if (dJ <= 0 || !((ds->lm[J] >> off) & 1ull) || (int64_t)J * CH_NB >= ds->ns) continue;
-        const int q = b.ngs++;
-        const int step = off + 1 < 64 ? __builtin_popcountll(ds->lm[J] >> (off + 1)) : 0;   // earlier launches
-        b.gs_J[q] = J;
-        b.gs_s[q] = ds->nslices - dJ + step;
-        b.gs_first[q] = step == 0;
-        const int64_t ni = ds->ns - (int64_t)J * CH_NB, nj = std::min<int64_t>(CH_NB, ni);
-        b.gs_cum[q + 1] = b.gs_cum[q] + cdiv(ni, 64) * cdiv(nj, 64);
-      }
-      b.gs_total = b.gs_cum[b.ngs];
-    }
-    // (IPM_FLEX=1: measured slower, 6.52 -> 7.14 ms at n = 8192 -- row chunks started beside the
-    // MFMA tiles run far slower than at the launch's end; kept as a knob)
-    b.flex = flex_on ? 1 : 0;
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.gs_total +
-                         b.rpad_a + b.rpad_b;
+    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
@@ -2275,64 +1928,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   }
 }
 
-static int num_cus();
-static int num_cus_host() { return num_cus(); }
-// ---- deferred KKT slices: the plan.  A Cholesky launch lasts at least the panel chain of its
-// 256-column block (~115 us); CUs idle beyond what its look-ahead tiles, row chunks and trailing
-// tiles occupy can take slices.  Capacity model per launch L (units = one 64 x 64 x 256 tile,
-// ~25 us of one workgroup slot): 2 slots per CU over the chain time, minus LA tiles (1 unit),
-// trailing 128-tiles (3.6) and row chunks (3), times a fill factor.  Slices are assigned column
-// by column (ascending J, each to the latest launch < J with room: earliest deadline first).
-static double env_d(const char* k, double dflt) {
-  const char* e = getenv(k);
-  return e && *e ? atof(e) : dflt;
-}
-int defer_ks() {
-  const int ks = (int)env_d("IPM_DEFER_KS", 256);
-  return ks >= 16 ? ks : 256;
-}
-int defer_plan(int64_t ns, int64_t m, int KS, int nblocks, int* d, unsigned long long* lm) {
-  for (int J = 0; J < nblocks; ++J) { d[J] = 0; lm[J] = 0; }
-  // opt-in (IPM_DEFER=1): measured on MI355X at n=8192 the up-front SYRK shrinks by exactly what
-  // the Cholesky launches grow (2.80 -> 2.53 ms vs 6.80 -> 7.07 ms): the CUs the chain leaves idle
-  // are not free capacity
-  if (env_d("IPM_DEFER", 0) == 0 || m <= 0 || KS <= 0 || nblocks < 2) return 0;
-  const int nslices = (int)std::min<int64_t>((m + KS - 1) / KS, 63);
-  const int64_t N = (int64_t)nblocks * CH_NB;           // rows of the factored matrix (approx.)
-  const double fill = env_d("IPM_DEFER_FILL", 0.6), chain_us = env_d("IPM_DEFER_CHAIN_US", 115);
-  const double ucost = env_d("IPM_DEFER_UNIT_US", 25) * 256.0 / KS;   // one 64-tile slice task
-  const int slots = 2 * num_cus();
-  std::vector<double> cap(nblocks, 0.0);
-  std::vector<int> jobs(nblocks, 0);
-  for (int L = 1; L < nblocks; ++L) {
-    const int64_t cb = (int64_t)L * CH_NB, r = std::max<int64_t>(N - cb, 0);
-    const double la = 4.0 * ((r + 63) / 64), T = (double)((std::max<int64_t>(r - CH_NB, 0) + 127) / 128);
-    const double busy = la + 3.6 * T * (T + 1) / 2 + 3.0 * 2 * ((r + 63) / 64);
-    cap[L] = std::max(0.0, fill * (slots * chain_us / 25.0 - busy));
-  }
-  const int maxj = std::min((int)env_d("IPM_DEFER_MAXJOBS", BlockArgs::MAXGS), (int)BlockArgs::MAXGS);
-  int pairs = 0;
-  for (int J = 2; J < nblocks && (int64_t)J * CH_NB < ns; ++J) {
-    const int64_t rows = ns - (int64_t)J * CH_NB;
-    const double need = ((rows + 63) / 64) * ((std::min<int64_t>(rows, CH_NB) + 63) / 64) * ucost / 25.0;
-    for (int L = J - 1; L >= 1 && d[J] < nslices && L >= J - 63; --L) {
-      if (cap[L] >= need && jobs[L] < maxj) {
-        cap[L] -= need;
-        ++jobs[L];
-        ++d[J];
-        lm[J] |= 1ull << (J - 1 - L);
-        ++pairs;
-      }
-    }
-  }
-  if (env_d("IPM_DEFER_PRINT", 0) != 0) {
-    fprintf(stderr, "defer plan ns=%lld m=%lld KS=%d pairs=%d\n", (long long)ns, (long long)m, KS, pairs);
-    for (int J = 0; J < nblocks; ++J)
-      fprintf(stderr, "  J=%2d d=%d lm=%llx jobs(L=J)=%d cap_left=%.0f\n", J, d[J], lm[J], jobs[J], cap[J]);
-  }
-  return pairs;
-}
-
 static int num_cus() {
   static int ncu = -1;
   if (ncu < 0) {
@@ -2342,94 +1937,6 @@ static int num_cus() {
   }
   return ncu;
 }
-// CUs kept free of trailing-update workgroups while a panel runs (IPM_PANEL_CUS, default 32; 0: off)
-static int panel_reserve_cus() {
-  static int r = -1;
-  if (r < 0) {
-    const char* e = getenv("IPM_PANEL_CUS");
-    r = e ? atoi(e) : 32;
-    if (r < 0 || r >= num_cus()) r = 0;
-  }
-  return r;
-}
-
-// Blocked right-looking Cholesky with one block of look-ahead.
-//   side stream: factor block k (two 128-wide panels + the GEMM between them)
-//   main stream: update block k+1's columns first, release it to the side stream, then the
-//                rest of the trailing matrix (SYRK, K = 256) -- overlapped with block k+1's panel.
-// Without a side stream (side == main) the same sequence runs in order.
-void potrf_lower_la(hipStream_t caller, const PotrfStreams* pst, int64_t n, double* A, int64_t lda, int* info,
-                    double* ws, int64_t ncols, const DeferSyrk* ds) {
-  // IPM_POTRF_LA=1: the earlier two-stream form below (kept for comparison); default: fused
-  static const bool two_stream = [] { const char* e = getenv("IPM_POTRF_LA"); return e && e[0] == '1'; }();
-  if (!two_stream || (ds && ds->active())) {
-    potrf_lower_fused(caller, n, A, lda, info, ws, ncols, ds);
-    return;
-  }
-  hipMemsetAsync(info, 0, sizeof(int), caller);
-  unsigned* ctl = reinterpret_cast<unsigned*>(ws + PF_DINV + 36 * 256);   // 4 words per panel
-  hipMemsetAsync(ctl, 0, 4 * sizeof(unsigned) * cdiv(std::max<int64_t>(n, 1), PF_NB), caller);
-  const bool two = pst && pst->side;
-  hipStream_t st = (two && pst->main) ? pst->main : caller;
-  hipStream_t side = two ? pst->side : caller;
-  hipEvent_t ev_rel = two ? pst->ev_rel : nullptr, ev_pan = two ? pst->ev_pan : nullptr;
-  if (st != caller) { hipEventRecord(pst->ev_in, caller); hipStreamWaitEvent(st, pst->ev_in, 0); }
-  if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
-  hipStream_t ps = two ? side : st;
-  static const bool la_side = [] { const char* e = getenv("IPM_LA_SIDE"); return e && e[0] == '1'; }();
-  for (int64_t k0 = 0; k0 < n; k0 += CH_NB) {
-    const int w = (int)std::min<int64_t>(CH_NB, n - k0);
-    // ---- panel k on the side stream
-    const int w1 = std::min(w, PF_NB);
-    const bool fold = w > w1 && fold_intra();
-    panel_launch(ps, n, k0, w1, A, lda, info, ws, ctl + 4 * (k0 / PF_NB), fold ? w - w1 : 0);
-    if (w > w1) {
-      // A[k0+w1 : n, k0+w1 : k0+w] -= L[k0+w1 : n, k0 : k0+w1] L[k0+w1 : k0+w, k0 : k0+w1]^T
-      if (!fold)
-        gemm_nt_sub_launch(ps, n - k0 - w1, w - w1, w1, A + k0 * lda + k0 + w1, lda, A + k0 * lda + k0 + w1, lda,
-                           A + (k0 + w1) * lda + k0 + w1, lda, info);
-      panel_launch(ps, n, k0 + w1, w - w1, A, lda, info, ws, ctl + 4 * ((k0 + w1) / PF_NB));
-    }
-    if (two) { hipEventRecord(ev_pan, side); hipStreamWaitEvent(st, ev_pan, 0); }
-    // ---- trailing update on the main stream
-    const int64_t r0 = k0 + w;
-    if (r0 >= n) break;
-    const int64_t w2 = std::min<int64_t>(CH_NB, n - r0);
-    // next block's columns (rectangle; its upper-triangle part is never read).  la_side: on the
-    // panel stream after the previous trailing update (ev_rel), so the next panel follows it
-    // without a stream hop.
-    if (two && la_side) {
-      hipStreamWaitEvent(side, ev_rel, 0);
-      gemm_nt_sub_launch(side, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0,
-                         lda, info);
-    } else {
-      gemm_nt_sub_launch(st, n - r0, w2, w, A + k0 * lda + r0, lda, A + k0 * lda + r0, lda, A + r0 * lda + r0, lda,
-                         info);
-      if (two) { hipEventRecord(ev_rel, st); hipStreamWaitEvent(side, ev_rel, 0); }
-    }
-    if (n - r0 - w2 > 0) {
-      GemmArgs a;
-      a.ni = a.nj = n - r0 - w2;
-      a.K = w;
-      a.X = a.Y = A + k0 * lda + r0 + w2;
-      a.ldx = a.ldy = lda;
-      a.C = A + (r0 + w2) * lda + r0 + w2;
-      a.ldc = lda;
-      a.alpha = -1.0;
-      a.beta = 1.0;
-      a.info = info;
-      a.tri = 1;
-      // with the look-ahead running: persistent form on all but panel_reserve_cus() CUs, one
-      // workgroup per CU, so the panel workgroups get CUs of their own (no fp64 MFMA neighbours)
-      const int res = panel_reserve_cus();
-      if (two && res > 0) mfma_gemm_launch_persistent(st, a, num_cus() - res);
-      else mfma_gemm_launch(st, a);
-    }
-    if (two && la_side) hipEventRecord(ev_rel, st);
-  }
-  if (st != caller) { hipEventRecord(pst->ev_out, st); hipStreamWaitEvent(caller, pst->ev_out, 0); }
-}
-
 #ifdef IPM_ROLE_TRACE
 extern "C" int ipm_debug_role_trace(unsigned long long* out, int n_wg) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_role_trace), sizeof(unsigned long long) * 4 *
@@ -2438,7 +1945,7 @@ extern "C" int ipm_debug_role_trace(unsigned long long* out, int n_wg) {
 #endif
 
 void potrf_lower(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws) {
-  potrf_lower_la(st, nullptr, n, A, lda, info, ws);
+  potrf_lower_fused(st, n, A, lda, info, ws);
 }
 
 // =====================================================================================

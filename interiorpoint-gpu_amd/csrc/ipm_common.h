@@ -48,11 +48,6 @@ struct SyrkEpi {
   int64_t ldp = 0;
   double tP = 0.0;
   const double* dvec = nullptr;
-  // per 256-column block K extent (deferred KKT slices): device table + its host copy (the host
-  // copy balances the tile runs of the 8 XCDs by work)
-  const int* kend_dev = nullptr;
-  const int* kend_host = nullptr;
-  int nkend = 0;
   // split tail (k_mfma_gemm_split): split_cap partial tiles of 128 x 128, then split_cap flags;
   // null: the plain tile grid
   double* split_ws = nullptr;
@@ -100,45 +95,11 @@ inline int64_t potrf_split_scratch_off(int64_t n) {
 inline int64_t potrf_ws_doubles(int64_t n) { return potrf_split_scratch_off(n) + potrf_split_cap(n) * 128 * 128; }
 void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws);
 
-// KKT SYRK slices deferred into the Cholesky (the Newton step's  H = tP + C^T diag(w) C + diag):
-// for 256-column block J the up-front SYRK stops at k row kend[J] = (nslices - d[J]) * KS and the
-// last d[J] slices of KS rows of C run inside d[J] of the Cholesky launches before J (one slice per
-// launch, lm[J]) as G(:, block J) (+)= C_s^T diag(w_s) C_s; the look-ahead tiles of launch J fold
-// G into block column J before its panel.  The slices fill CUs the panel chain leaves idle.
-struct DeferSyrk {
-  const double* X = nullptr;   // C: m x ns row-major (ldx), 16-byte aligned, ldx even
-  int64_t ldx = 0;
-  const double* w = nullptr;   // weights (m)
-  int64_t m = 0, ns = 0;       // rows of C, SYRK dimension (columns of H it covers)
-  double* G = nullptr;         // deferred partial sums, column-major (ldg), ns x ns
-  int64_t ldg = 0;
-  int KS = 256;                // k rows per slice
-  int nslices = 0;             // ceil(m / KS)
-  int nblocks = 0;             // 256-column blocks with an entry in d
-  const int* d = nullptr;      // [host] deferred slice count per block (d[0] == d[1] == 0)
-  const unsigned long long* lm = nullptr;   // [host] launches carrying block J's slices: bit J-1-L
-  const int* kend = nullptr;   // [device] up-front K extent per block
-  bool active() const { return G && d && nblocks > 0; }
-};
-// planner: fills d[0..nblocks) (host) from the sizes and the IPM_DEFER* knobs; returns the
-// number of deferred (block, slice) pairs (0: nothing deferred)
-int defer_plan(int64_t ns, int64_t m, int KS, int nblocks, int* d, unsigned long long* lm);
-int defer_ks();   // k rows per deferred slice (IPM_DEFER_KS, default 256)
-// one launch per 256-column block on stream s (the default behind potrf_lower / potrf_lower_la).
+// Blocked right-looking Cholesky, one launch per 256-column block on stream s (k_potrf_block).
 // ncols < n: only the first ncols columns are factored (all n rows) -- the bordered Newton system
 // needs row n-1 of L (the forward-solved right-hand side) but not its diagonal entry.
 void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws,
-                       int64_t ncols = -1, const DeferSyrk* ds = nullptr);
-// default: potrf_lower_fused on s.  IPM_POTRF_LA=1: the earlier two-stream form -- panels on
-// ps->side (high priority), trailing updates on ps->main, events between them (ps == null or
-// ps->side == null: everything in order on s; ncols is ignored there).  The call is ordered
-// after earlier work on s, and later work on s is ordered after it.
-struct PotrfStreams {
-  hipStream_t main = nullptr, side = nullptr;
-  hipEvent_t ev_rel = nullptr, ev_pan = nullptr, ev_in = nullptr, ev_out = nullptr;
-};
-void potrf_lower_la(hipStream_t s, const PotrfStreams* ps, int64_t n, double* H, int64_t ldh, int* info_dev,
-                    double* ws, int64_t ncols = -1, const DeferSyrk* ds = nullptr);
+                       int64_t ncols = -1);
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,

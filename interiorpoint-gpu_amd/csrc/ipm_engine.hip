@@ -85,17 +85,8 @@ struct ipm_problem {
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
   bool use_backup = false;
   bool pieces_valid = false;  // barrier pieces (inv/coef/G) match the current slack state
-  // KKT SYRK slices deferred into the Cholesky (DeferSyrk, ipm_common.h); LP/QP Cholesky path
-  std::vector<int> defer_d;   // per 256-column block; empty: no deferral
-  std::vector<unsigned long long> defer_lm;
-  std::vector<int> kend_h;
-  int64_t defer_pairs = 0;
-  int* kend_d = nullptr;
-  double* Gd = nullptr;
   double* sws = nullptr;   // KKT SYRK split tail (syrk_split_ws_doubles)
   double* lsw = nullptr;   // least-squares workspace (lstsq_ws_doubles; null when the method never uses it)
-  DeferSyrk dsy;
-  bool defer_on = false;
 };
 
 // ------------------------------------------------------------------------- workspace
@@ -142,21 +133,6 @@ void derive(ipm_problem* pr) {
   }
   // room for one bordered row (N+1 rows): the Newton right-hand side rides through the Cholesky
   pr->ldh = (pr->N + 1) + ((pr->N + 1) & 1);
-  // deferred KKT slices (sizes only; alignment is checked at problem creation)
-  pr->defer_d.clear();
-  pr->defer_lm.clear();
-  pr->defer_pairs = 0;
-  if (!pr->socp && pr->m > 0 && !pr->diag && !pr->lu) {
-    const int nb = (int)((pr->N + 255) / 256);
-    std::vector<int> dv(nb, 0);
-    std::vector<unsigned long long> lm(nb, 0);
-    const int64_t pairs = defer_plan(pr->n, pr->m, defer_ks(), nb, dv.data(), lm.data());
-    if (pairs > 0) {
-      pr->defer_d = dv;
-      pr->defer_lm = lm;
-      pr->defer_pairs = pairs;
-    }
-  }
 }
 
 int64_t carve(ipm_problem* pr, char* base) {
@@ -240,11 +216,6 @@ int64_t carve(ipm_problem* pr, char* base) {
   }
   pr->rowcone_d = c.take<int64_t>(pr->R + 1);
   pr->dslot_d = c.take<int64_t>(pr->K + 1);
-  if (!pr->defer_d.empty()) {
-    const int64_t ldg = n + (n & 1);
-    pr->Gd = c.take<double>(ldg * n);
-    pr->kend_d = c.take<int>((int64_t)pr->defer_d.size());
-  }
   return c.off + 256;
 }
 
@@ -370,7 +341,7 @@ void assemble_barrier_grad(ipm_problem* pr, double* B) {
 // Hessian into H (column-major lower, ldh) -- or the diagonal vector hdiag for the
 // diagonal strategy.  Requires barrier_pieces at the same slack state.
 // (FunctionManager.py:267-326, 547-611, 783-827, 1104-1158, 1372-1453)
-void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool defer = false) {
+void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
   const ipm_problem_desc& d = pr->d;
   hipStream_t st = S(pr);
   const double add = psd ? 1e-9 : 0.0;
@@ -392,13 +363,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd, bool
       if (pr->qp) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     }
     e.dvec = pr->dvec;
-    // defer: columns ahead stop at kend (their last slices run inside the Cholesky)
-    if (defer) {
-      e.kend_dev = pr->kend_d;
-      e.kend_host = pr->kend_h.data();
-      e.nkend = (int)pr->kend_h.size();
-    }
-    if (!defer && pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
+    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
     syrk_lower(st, pr->n, pr->m, 1.0, d.C, d.ldc, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // border: hxs = -C^T inv_C^2 + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (+psd)
@@ -457,25 +422,6 @@ extern "C" int ipm_create(int device, void* stream, ipm_handle** out) {
   // NULL = the legacy default stream (what torch's default stream is), so work is ordered
   // with the caller's tensor initialisation and reads without extra events.
   h->stream = (hipStream_t)stream;
-  {
-    int least = 0, greatest = 0;
-    hipDeviceGetStreamPriorityRange(&least, &greatest);
-    // IPM_NO_LOOKAHEAD=1: Cholesky on the caller's stream only (debug).  Otherwise panels run on
-    // a high-priority side stream, trailing updates on the caller's stream.  (CU-masked streams
-    // were tried: hipExtStreamCreateWithCUMask is not honoured on this platform -- a probe
-    // kernel on a 32-CU-masked stream still ran on all 256 CUs.)
-    const char* nola = getenv("IPM_NO_LOOKAHEAD");
-    PotrfStreams& ps = h->pst;
-    if (!(nola && nola[0] == '1') &&
-        hipStreamCreateWithPriority(&ps.side, hipStreamNonBlocking, greatest) != hipSuccess)
-      ps.side = nullptr;
-    const char* nf = getenv("IPM_EV_NOFENCE");
-    const unsigned evf = hipEventDisableTiming | ((nf && nf[0] == '1') ? hipEventDisableSystemFence : 0u);
-    hipEventCreateWithFlags(&ps.ev_rel, evf);
-    hipEventCreateWithFlags(&ps.ev_pan, evf);
-    hipEventCreateWithFlags(&ps.ev_in, evf);
-    hipEventCreateWithFlags(&ps.ev_out, evf);
-  }
   if (hipHostMalloc((void**)&h->hbuf, HOST_WORDS * sizeof(double)) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   if (hipMalloc((void**)&h->dinfo, 64) != hipSuccess) { delete h; return IPM_HIP_ERROR; }
   h->ctl = reinterpret_cast<unsigned*>(h->dinfo + 8);
@@ -493,10 +439,6 @@ extern "C" int ipm_destroy(ipm_handle* h) {
   if (h->scratch) hipFree(h->scratch);
   lstsq_release(h->rb);
   for (auto& ev : h->ev) hipEventDestroy(ev);
-  for (hipEvent_t e : {h->pst.ev_rel, h->pst.ev_pan, h->pst.ev_in, h->pst.ev_out})
-    if (e) hipEventDestroy(e);
-  if (h->pst.side) hipStreamDestroy(h->pst.side);
-  if (h->pst.main) hipStreamDestroy(h->pst.main);
   if (h->own_stream) hipStreamDestroy(h->stream);
   delete h;
   return IPM_OK;
@@ -549,7 +491,7 @@ extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double
     HIPCHK(h, hipMalloc((void**)&h->pws, potrf_ws_doubles(n) * sizeof(double)));
     h->pws_n = n;
   }
-  potrf_lower_la(h->stream, &h->pst, n, H, ldh, h->dinfo, h->pws, ncols);
+  potrf_lower_fused(h->stream, n, H, ldh, h->dinfo, h->pws, ncols);
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;
@@ -646,24 +588,13 @@ extern "C" int ipm_last_timings(ipm_handle* h, double* kkt_ms, double* potrf_ms,
 }
 
 extern "C" int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred) {
-  // KKT SYRK flops (SYRK convention: 2 per multiply-add over the lower triangle incl. diagonal)
-  // split between the up-front SYRK kernel and the slices deferred into the Cholesky
+  // KKT SYRK flops (SYRK convention: 2 per multiply-add over the lower triangle incl. diagonal);
+  // all of it runs in the up-front SYRK kernel (deferred: 0, kept for ABI compatibility)
   if (!pr) return IPM_INVALID_ARG;
   const double n = (double)pr->n;
   const double m = (double)(pr->socp ? pr->XR : pr->m);
-  double def = 0.0;
-  if (pr->defer_on) {
-    const DeferSyrk& ds = pr->dsy;
-    for (int J = 0; J < ds.nblocks; ++J) {
-      const int64_t c0 = (int64_t)J * 256;
-      if (ds.d[J] <= 0 || c0 >= ds.ns) continue;
-      const double w = (double)std::min<int64_t>(256, ds.ns - c0), r = (double)(ds.ns - c0);
-      const double krows = (double)(ds.m - (int64_t)(ds.nslices - ds.d[J]) * ds.KS);
-      def += krows * (w * r - w * (w - 1) / 2.0) * 2.0;   // lower part of block column J
-    }
-  }
-  if (upfront) *upfront = m * n * (n + 1) - def;
-  if (deferred) *deferred = def;
+  if (upfront) *upfront = m * n * (n + 1);
+  if (deferred) *deferred = 0.0;
   return IPM_OK;
 }
 
@@ -773,29 +704,6 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
   carve(pr, reinterpret_cast<char*>(workspace));
   hipMemsetAsync(pr->info, 0, RB_MASK, h->stream);   // info words incl. the sticky device error word
   pr->use_backup = d.solve_method == IPM_SOLVE_LU || d.solve_method == IPM_SOLVE_LSTSQ;
-  if (!pr->defer_d.empty() && (d.ldc & 1) == 0 && (((uintptr_t)d.C) & 15) == 0) {
-    // deferred KKT slices: the up-front K extent per block, uploaded once
-    DeferSyrk& ds = pr->dsy;
-    ds.X = d.C;
-    ds.ldx = d.ldc;
-    ds.w = pr->w;
-    ds.m = pr->m;
-    ds.ns = pr->n;
-    ds.G = pr->Gd;
-    ds.ldg = pr->n + (pr->n & 1);
-    ds.KS = defer_ks();
-    ds.nslices = (int)((pr->m + ds.KS - 1) / ds.KS);
-    ds.nblocks = (int)pr->defer_d.size();
-    ds.d = pr->defer_d.data();
-    ds.lm = pr->defer_lm.data();
-    std::vector<int> kend(pr->defer_d.size());
-    for (size_t J = 0; J < kend.size(); ++J) kend[J] = (ds.nslices - pr->defer_d[J]) * ds.KS;
-    HIPCHK(h, hipMemcpyAsync(pr->kend_d, kend.data(), kend.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    pr->kend_h = kend;
-    ds.kend = pr->kend_d;
-    pr->defer_on = true;
-  }
   if (pr->socp) {
     // host-side structure: row -> cone, cone -> diagonal slot
     pr->rowcone_h.assign(pr->R + 1, 0);
@@ -1084,8 +992,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     hipMemsetAsync(pr->info, 0, sizeof(int), st);
     return IPM_OK;
   }
-  const bool defer = pr->defer_on && !pr->use_backup;
-  assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0, defer);
+  assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
   if (!pr->use_backup) {
     // Cholesky of the bordered [[H, -g], [-g^T, big]]: its last row is y = L^-1 (-g) (the forward
     // solve of NewtonSolver.py:287-299 / cho_solve), then one backward solve L^T dx = y
@@ -1093,7 +1000,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
     // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
-    potrf_lower_la(st, &h->pst, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, defer ? &pr->dsy : nullptr);
+    potrf_lower_fused(st, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N);
     if (h->timing) hipEventRecord(h->ev[3], st);
     trsv_lower_t(st, pr->N, pr->H, pr->ldh, pr->H + pr->N, pr->ldh, pr->dx, pr->ctl, pr->xinv, trsv_err(pr));
   } else if (!pr->lu) {
@@ -1220,7 +1127,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
   const int64_t lds = p + (p & 1);
   if (!pr->use_backup) {
-    potrf_lower_la(st, &pr->h->pst, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
+    potrf_lower_fused(st, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g
     copy(st, pr->Ybuf, d.AT, n * p);
     if (p >= 32 && n >= 128) {

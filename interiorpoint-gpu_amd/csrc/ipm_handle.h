@@ -12,7 +12,6 @@ constexpr int IPM_HOST_WORDS = 4096;   // pinned host staging (doubles)
 struct ipm_handle {
   int device = 0;
   hipStream_t stream = nullptr;
-  ipm::PotrfStreams pst;                  // Cholesky look-ahead: panel / trailing streams (CU-masked)
   bool own_stream = false;
   std::string err;
   double* hbuf = nullptr;  // pinned host staging

@@ -65,50 +65,16 @@ struct GemmArgs {
   int rowmajor = 0;              // tile L -> (L / tiles_j, L % tiles_j) (no remap): row blocks in order
   int64_t tiles_i = 0, tiles_j = 0, nblk = 0;
   int accum = 0;                 // C += alpha-free sum (accumulators start from C, P/dvec ignored)
-  const int* kend256 = nullptr;  // per 256-column block of the tile's column: K extent (<= K)
-  const double* C2 = nullptr;    // sub/accum, FOLD instantiations: + C2(i, j) (i, j < n2) in the start value
-  int64_t ldc2 = 0, n2 = 0, n2c = 0;   // C2 rows / columns (relative to the tile origin)
-  int xbal = 0;                  // blockIdx b -> tile xb[b % 8] + b / 8 (runs of equal work per XCD)
-  int xb[9] = {};
-  int sb = 0;                    // tri grids (KKT SYRK): super-block order, sb x sb tiles (0: row order);
-                                 // applied by the kernels before mfma_tile (tri_sb_index), xcd_remap = 0
 };
 
-// Super-block order of a lower-triangle tile grid (GemmArgs::sb = S): the XCD-contiguous run of
-// enumeration index Lw (the same remap as xcd_remap), then super-rows of S tile rows in order,
-// inside a super-row the S x S blocks left to right (row-major inside a block) and the triangular
-// diagonal block last.  The 2 x 32 workgroups an XCD runs at once then cover one S = 8 block: 8 X
-// and 8 Y operand panels between them instead of 1 X panel and 64 Y panels (the row order's tile
-// run), so the panels' slabs are L2 hits.  Returns the plain row-order index bi (bi + 1) / 2 + bj
-// that mfma_tile / tile_ij decode.  A bijection on [0, nblk).
-__device__ __forceinline__ int64_t tri_sb_index(const GemmArgs& a, int64_t Lw) {
-  const int64_t S = a.sb, T = a.tiles_i, q = a.nblk >> 3;
-  int64_t L = Lw;
-  if (L < (q << 3)) L = (L & 7) * q + (L >> 3);
-  int64_t Bi = 0, base = 0, r = 0;
-  for (;;) {
-    r = std::min<int64_t>(S, T - S * Bi);
-    const int64_t cnt = Bi * r * S + r * (r + 1) / 2;
-    if (L < base + cnt || r <= 0) break;
-    base += cnt;
-    ++Bi;
-  }
-  const int64_t u = L - base;
-  int64_t bi, bj;
-  if (u < Bi * r * S) {
-    const int64_t Bj = u / (r * S), v = u - Bj * r * S;
-    bi = S * Bi + v / S;
-    bj = S * Bj + v % S;
-  } else {
-    const int64_t w = u - Bi * r * S;
-    int64_t row = (int64_t)((sqrt(8.0 * (double)w + 1.0) - 1.0) * 0.5);
-    while ((row + 1) * (row + 2) / 2 <= w) ++row;
-    while (row * (row + 1) / 2 > w) --row;
-    bi = S * Bi + row;
-    bj = S * Bi + (w - row * (row + 1) / 2);
-  }
-  return bi * (bi + 1) / 2 + bj;
-}
+// A kernel's FIRST (struct) parameter read through the kernarg segment pointer where it is used:
+// as a by-value parameter every field is loaded at kernel entry by the argument lowering and the
+// whole struct stays live in SGPRs across the kernel (the Cholesky kernel spilled 100-300 SGPRs to
+// VGPR lanes for it).  The parameter stays declared (it defines the kernarg layout: offset 0).
+// (On the GEMM kernels the same change cost the KKT SYRK 1-1.5 %, r5b: not used there.)
+#define IPM_KARGS(T, name, param) \
+  (void)param;                    \
+  const T& name = *(const T*)__builtin_amdgcn_kernarg_segment_ptr()
 
 // agent-coherent (sc1) element access: data handed between workgroups of ONE launch
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -160,9 +126,6 @@ __device__ __forceinline__ bool spin_until(int* info, unsigned* failw, Done done
 
 // BM = 128 (4 x 4 MFMA tiles per wave) for large grids, 64 (2 x 2) when the 128-tile grid
 // would leave CUs idle.  WJ = waves along j (2: 256 threads, 2 workgroups per CU; 4: 512 threads).
-// PAD > 0 pads the LDS allocation so that only ONE workgroup fits a CU and no Cholesky panel
-// workgroup (77 KB) can share it: the persistent trailing-update form (grid = CUs left to it,
-// each workgroup loops over tiles), which keeps a set of CUs free for the panel stream.
 template <int BM_, int WJ = 2>
 struct MfCfg {
   static constexpr int BM = BM_, BK = 16, NT = 128 * WJ;
@@ -184,8 +147,6 @@ struct alignas(16) MfSmem {
 
 // One output tile (index Lw of the launch's tile space) by one workgroup of 128 * WJ threads.
 // SC1OUT: the tile is stored with sc1 stores (read by other workgroups of the same launch).
-// FOLD: a.C2 is folded into the start value (the Cholesky look-ahead tiles taking the deferred
-// KKT slices); a separate instantiation keeps the other tiles' register budget.
 // split (Cholesky trailing tiles of a launch's last round, sub tiles only): the K range is cut in
 // two halves computed by two workgroups at once.  SPLIT 1 (the LOWER ticket): k in [K/2, K), the
 // accumulators start at 0, the tile -X^T Y goes to the scratch tile `part` (sc1, 128 x 128
@@ -201,8 +162,8 @@ struct alignas(16) MfSmem {
 // C tile is read one 16 x 16 MFMA block per slab (two slabs ahead of its add), so the 128 KB C read
 // is spread over the K loop instead of a burst before the first MFMA (all workgroups of a round
 // start together: the burst is bandwidth-bound).  C + sum(products) in another association order.
-template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool FOLD = false, bool SPLITADD = false,
-          int LOOP = 0, int LAZYC = 0, bool CST = false>
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, bool SC1OUT = false, bool SPLITADD = false, int LOOP = 0,
+          int LAZYC = 0, bool CST = false>
 __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<BM_, WJ>& sm, int SPLIT = 0,
                                           double* part = nullptr, unsigned* pflag = nullptr, int64_t kb = -1,
                                           int64_t ke = -1, int* sinfo = nullptr, unsigned* failw = nullptr) {
@@ -217,7 +178,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   {
     int64_t L = Lw;
     const int64_t q = a.nblk >> 3;
-    if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
+    if (a.xcd_remap && !a.rowmajor && L < (q << 3)) L = (L & 7) * q + (L >> 3);   // XCD-contiguous tile runs
     if (a.rowmajor) {
       bi = L / a.tiles_j;
       bj = L % a.tiles_j;
@@ -243,16 +204,14 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   const double* xp = a.X + (sr + kbeg) * a.ldx + I0 + sc;
   const double* yp = a.Y + (sr + kbeg) * a.ldy + J0 + sc;
   const int64_t xstep = BK * a.ldx, ystep = BK * a.ldy;
-  // K extent of this tile (the KKT SYRK with deferred slices: columns ahead take fewer k rows)
   int kt32 = (int)a.K;
-  if (a.kend256) kt32 = __builtin_amdgcn_readfirstlane(std::min(kt32, a.kend256[J0 >> 8]));
   if (SPLIT == 1) kt32 = kpiece ? (int)(ke - kb) : kt32 - kt32 / 2;
   if (SPLIT == 2) kt32 = kt32 / 2;
   const int64_t Kt = kt32;
   const int64_t nslab = (Kt + BK - 1) / BK;
   // C -= X^T Y (Cholesky updates): the accumulators start FROM the C tile (its loads overlap the
   // first slab's) and X is staged negated -- no dependent C read in the epilogue.  accum: the
-  // same with C += X^T diag(w) Y (the deferred KKT slices).
+  // same with C += X^T diag(w) Y.
   const bool cinit = a.sub || a.accum || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
   const double xsg = (cinit && !a.accum) ? -1.0 : 1.0;
   double rx[PT], ry[PT];
@@ -303,11 +262,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   for (int u = 0; u < TWJ; ++u)
 #pragma unroll
     for (int v = 0; v < TWI; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
-  static_assert(!LAZYC || (LOOP == 1 && !FOLD && !WEIGHT ), "lazy C: fast loop, no fold, no weight");
+  static_assert(!LAZYC || (LOOP == 1 && !WEIGHT), "lazy C: fast loop, no weight");
   // CST (LOOP 1 full tiles, C -= X^T Y): the C tile moves through LDS in two 64-column halves --
   // each wave instruction reads / writes 4 whole 1 KB tile columns instead of 128-byte pieces
   // in four columns (the MFMA accumulator layout) -- before the first slab and after the last
-  static_assert(!CST || (LOOP == 1 && !FOLD && !LAZYC && BM_ == 128 && WJ == 2), "staged C: 128-tile fast loop");
+  static_assert(!CST || (LOOP == 1 && !LAZYC && BM_ == 128 && WJ == 2), "staged C: 128-tile fast loop");
   constexpr int CLD = 144;   // staged column stride (doubles): 2 CLD = 32 (mod 64) dwords
   double* sCst = &sm.sX[0][0];   // sX, sY contiguous: 4 * BK * LD = 64 * CLD doubles
   static_assert(!CST || 4 * BK * LD >= 64 * CLD, "staging fits the slab buffers");
@@ -341,9 +300,7 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
-          double v = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
-          if (FOLD && i < a.n2 && j < a.n2c) v += a.C2[j * a.ldc2 + i];
-          acc[tj][ti][r] = v;
+          acc[tj][ti][r] = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
         }
       }
   }
@@ -587,12 +544,12 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
 }
 
 // the tile mfma_tile would take for index Lw (same enumeration), and whether it is full with whole
-// 16-row K slabs (no kend / split pieces: callers of the fast loop)
+// 16-row K slabs (no split pieces: callers of the fast loop)
 template <int BM>
 __device__ __forceinline__ bool tile_fast_ok(const GemmArgs& a, int64_t Lw) {
   int64_t L = Lw, bi, bj;
   const int64_t q = a.nblk >> 3;
-  if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);
+  if (a.xcd_remap && !a.rowmajor && L < (q << 3)) L = (L & 7) * q + (L >> 3);
   if (a.rowmajor) {
     bi = L / a.tiles_j;
     bj = L % a.tiles_j;
@@ -606,29 +563,16 @@ __device__ __forceinline__ bool tile_fast_ok(const GemmArgs& a, int64_t Lw) {
     bi = L % a.tiles_i;
     bj = L / a.tiles_i;
   }
-  return (bi + 1) * BM <= a.ni && (bj + 1) * BM <= a.nj && (a.K % 16) == 0 && a.kend256 == nullptr;
+  return (bi + 1) * BM <= a.ni && (bj + 1) * BM <= a.nj && (a.K % 16) == 0;
 }
 
-template <int BM_, bool WEIGHT, bool VEC, int WJ = 2, int PAD = 0>
+template <int BM_, bool WEIGHT, bool VEC, int WJ = 2>
 __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a) {
   if (a.info && *a.info != 0) return;
   __shared__ MfSmem<BM_, WJ> sm;
-  __shared__ double spad[PAD > 0 ? PAD : 1];
-  if (PAD > 0 && a.ni < 0) spad[threadIdx.x] = 0.0;   // never executed: keeps the pad allocated
-  if (a.xbal) {
-    // work-balanced XCD runs (constant-index selects: no dynamically indexed argument array)
-    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      if (i == x) { s0 = a.xb[i]; s1 = a.xb[i + 1]; }
-    if (s0 + l < s1) mfma_tile<BM_, WEIGHT, VEC, WJ>(a, s0 + l, sm);
-    return;
-  }
-  for (int64_t Lb = blockIdx.x; Lb < a.nblk; Lb += gridDim.x) {
-    const int64_t Lw = a.sb ? tri_sb_index(a, Lb) : Lb;
+  for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
     if (BM_ == 128 && VEC && WJ == 2 && tile_fast_ok<BM_>(a, Lw))
-      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, false, (BM_ == 128 && VEC && WJ == 2) ? 1 : 0>(a, Lw, sm);
+      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, (BM_ == 128 && VEC && WJ == 2) ? 1 : 0>(a, Lw, sm);
     else
       mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
   }
@@ -648,18 +592,17 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t 
   const int64_t b = blockIdx.x;
   constexpr int FL = (BM_ == 128 && VEC) ? 1 : 0;
   if (b < s_full) {
-    const int64_t Lw = a.sb ? tri_sb_index(a, b) : b;
-    if (FL && tile_fast_ok<BM_>(a, Lw)) mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, Lw, sm);
-    else mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, Lw, sm);
+    if (FL && tile_fast_ok<BM_>(a, b)) mfma_tile<BM_, WEIGHT, VEC, 2, false, true, FL>(a, b, sm);
+    else mfma_tile<BM_, WEIGHT, VEC, 2, false, true>(a, b, sm);
     return;
   }
   const int64_t u = b - s_full, p = u >> 1;
   double* part = sscr + p * (int64_t)(BM_ * BM_);
-  const int64_t Lw = a.sb ? tri_sb_index(a, s_full + p) : s_full + p;
+  const int64_t Lw = s_full + p;
   if (FL && (a.K % 32) == 0 && tile_fast_ok<BM_>(a, Lw))
-    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true, FL>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, true, FL>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
   else
-    mfma_tile<BM_, WEIGHT, VEC, 2, false, false, true>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
+    mfma_tile<BM_, WEIGHT, VEC, 2, false, true>(a, Lw, sm, (u & 1) ? 2 : 1, part, sflag + p);
 }
 
 // Stream-K tail (the KKT SYRK on 128-tiles): a lower-triangle grid of nt = R * slots + q tiles
@@ -675,7 +618,7 @@ template <int BM>
 __device__ __forceinline__ void tile_ij(const GemmArgs& a, int64_t Lw, int64_t& bi, int64_t& bj) {
   int64_t L = Lw;
   const int64_t q = a.nblk >> 3;
-  if (a.xcd_remap && !a.rowmajor && !a.xbal && L < (q << 3)) L = (L & 7) * q + (L >> 3);
+  if (a.xcd_remap && !a.rowmajor && L < (q << 3)) L = (L & 7) * q + (L >> 3);
   if (a.rowmajor) {
     bi = L / a.tiles_j;
     bj = L % a.tiles_j;
@@ -710,20 +653,20 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
     whole = b >= npc;
   }
   if (whole) {
-    const int64_t L = a.sb ? tri_sb_index(a, pieces_last ? b : b - npc) : (pieces_last ? b : b - npc);
-    if (FL && tile_fast_ok<BM>(a, L)) mfma_tile<BM, WEIGHT, VEC, 2, false, false, true, FL>(a, L, sm);
-    else mfma_tile<BM, WEIGHT, VEC, 2, false, false, true>(a, L, sm);
+    const int64_t L = pieces_last ? b : b - npc;
+    if (FL && tile_fast_ok<BM>(a, L)) mfma_tile<BM, WEIGHT, VEC, 2, false, true, FL>(a, L, sm);
+    else mfma_tile<BM, WEIGHT, VEC, 2, false, true>(a, L, sm);
     return;
   }
-  const int64_t ti = b / P, p = b - ti * P, L = a.sb ? tri_sb_index(a, s_full + ti) : s_full + ti;
+  const int64_t ti = b / P, p = b - ti * P, L = s_full + ti;
   const int64_t k0 = p * Kp, k1 = std::min<int64_t>(a.K, k0 + Kp);
   double* part = sscr + b * (int64_t)(BM * BM);
   // (the flag mfma_tile raises after its partial: a per-piece word past the tile counters)
   unsigned* pf = cnt + (a.nblk - s_full) + b;
   if (FL && (k0 % 16) == 0 && ((k1 - k0) % 16) == 0 && tile_fast_ok<BM>(a, L))
-    mfma_tile<BM, WEIGHT, VEC, 2, false, false, true, FL>(a, L, sm, 1, part, pf, k0, k1);
+    mfma_tile<BM, WEIGHT, VEC, 2, false, true, FL>(a, L, sm, 1, part, pf, k0, k1);
   else
-    mfma_tile<BM, WEIGHT, VEC, 2, false, false, true>(a, L, sm, 1, part, pf, k0, k1);
+    mfma_tile<BM, WEIGHT, VEC, 2, false, true>(a, L, sm, 1, part, pf, k0, k1);
   // (mfma_tile ended with s_waitcnt vmcnt(0) + barrier after the partial's sc1 stores)
   const int tid = threadIdx.x;
   if (tid == 0)
@@ -842,21 +785,6 @@ inline void mfma_gemm_launch_bm(hipStream_t st, GemmArgs a, bool vec) {
     if (vec) hipLaunchKernelGGL((k_mfma_gemm<BM, false, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_mfma_gemm<BM, false, false>), g, b, 0, st, a);
   }
-}
-
-// persistent one-workgroup-per-CU form (no weight): at most `max_wg` workgroups loop over the
-// 128-tiles; used for the Cholesky trailing update while the panel stream owns the other CUs
-inline void mfma_gemm_launch_persistent(hipStream_t st, GemmArgs a, int max_wg) {
-  if (a.ni <= 0 || a.nj <= 0) return;
-  const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
-                   ((((uintptr_t)a.Y) & 15) == 0);
-  const int64_t ti = (a.ni + 127) / 128, tj = (a.nj + 127) / 128;
-  a.tiles_i = ti;
-  a.nblk = a.tri ? ti * (ti + 1) / 2 : ti * tj;
-  dim3 g((unsigned)std::min<int64_t>(a.nblk, max_wg)), b(512);
-  constexpr int PAD = 2200;   // 73.7 + 17.6 KB: one per CU, and no 77 KB panel workgroup beside it
-  if (vec) hipLaunchKernelGGL((k_mfma_gemm<128, false, true, 4, PAD>), g, b, 0, st, a);
-  else hipLaunchKernelGGL((k_mfma_gemm<128, false, false, 4, PAD>), g, b, 0, st, a);
 }
 
 // launch helper: picks the tile size (grid fill), the weighted / vector-load instantiation

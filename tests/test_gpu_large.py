@@ -354,6 +354,45 @@ def test_m5_socp_full_solve():
         np.testing.assert_array_equal(gs, z["trace_step"])
 
 
+@pytest.mark.parametrize("name", ["m5ref_socp_n256", "m5ref_socp_n2048"])
+def test_m5ref_socp_full_solve(name):
+    """Config 5's cone shape pinned to the REFERENCE itself: SOCPSolver with
+    K=256 cones of 16 rows, P=I, strictly feasible x0, SOCP_KWARGS (testSolver.py:924-945), at
+    n=2048 (and n=256) where the reference's 2 K n^2 cone caches fit the build container
+    (FunctionManager.py:869-894, 1104-1158; tests/golden/make_golden_m5ref.py).  Bars as for the M3
+    full solves: x* within max(1e-6, 4x the reference's 1e-15-perturbation spread), the value
+    likewise; where the reference's step sequence is stable under that perturbation, identical
+    inner iteration counts and every accepted step size identical."""
+    import ast as _ast
+    import ipm355
+    from ipm355 import problems
+    z = _fixture(name)
+    spec = _ast.literal_eval(str(z["spec"]))
+    inst = problems.socp_cones(n=spec["n"], K=spec["K"], mi=spec["mi"], seed=spec["seed"])
+    x0 = inst.pop("x0")
+    dg = problems.input_digest({"A": np.stack(inst["A"]), "b": np.stack(inst["b"]), "c": np.stack(inst["c"]),
+                                "q": inst["q"]})
+    assert dg == str(z["digest"])
+    inst["d"] = [float(v) for v in z["d"]]
+    kw = _ast.literal_eval(str(z["kwargs"]))
+    g = ipm355.SOCPSolver(check_cvxpy=False, suppress_print=True, x0=x0.copy(), **inst, **kw)
+    v = g.solve()
+    err = rel(g.xstar, z["xstar"])
+    gs = np.array([t[0] for t in g.ns.trace])
+    xtol = max(XSTAR_RTOL, 4 * float(z["sens_xstar_rel"]))
+    ref = z["trace_step"]
+    k = min(len(gs), len(ref))
+    first = int(np.argmax(gs[:k] != ref[:k])) if np.any(gs[:k] != ref[:k]) else k
+    print(f"[{name}] x* rel {err:.2e} (tol {xtol:.1e}), value {v!r} vs {float(z['value'])!r}, iters "
+          f"{list(g.inner_iters)} vs reference {list(z['inner_iters'])}, reference stable "
+          f"{bool(z['sens_steps_stable'])}, first differing step {first} of {k}")
+    assert err <= xtol
+    assert abs(v - float(z["value"])) <= max(1e-8, 4 * float(z["sens_value_rel"])) * abs(float(z["value"]))
+    if bool(z["sens_steps_stable"]):
+        assert list(g.inner_iters) == list(z["inner_iters"])
+        np.testing.assert_array_equal(gs, ref)
+
+
 def test_m5_socp_against_oracle():
     """M5: SOCPSolver n=4096, K=256 cones of 16 rows, P=I, strictly feasible x0 (phase 1 skipped):
     the first centering step truncated to 3 Newton steps on the device and in the oracle."""

@@ -258,41 +258,6 @@ def test_concurrent_instances_match_sequential():
         np.testing.assert_array_equal(np.array(s.xstar), ref)
 
 
-@pytest.mark.parametrize("knobs", [
-    {"IPM_DEFER_KS": "256"},
-    {"IPM_DEFER_KS": "64"},
-    {"IPM_DEFER_KS": "48", "IPM_DEFER_MAXJOBS": "2"},
-])
-def test_deferred_kkt_slices_match(knobs, monkeypatch):
-    """KKT-SYRK slices deferred into the Cholesky launches (DeferSyrk): the same QP solve (phase 1
-    included, bordered right-hand side) with the deferral forced at n=1030 (5 blocks of 256, a
-    ragged last block and slice) against the undeferred solve and the oracle: x* within 1e-6 of
-    the oracle; the summation order changes, so the trajectories are compared to the oracle's
-    tolerance rather than bit for bit."""
-    import ipm355
-    from ipm355 import problems
-    from oracle import ipm_oracle as O
-    kw = dict(problems.qp_ineq_box(1030, 300, seed=4), **problems.QP_KWARGS)
-    monkeypatch.delenv("IPM_DEFER", raising=False)          # default: off
-    ref = ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw)
-    v_ref = ref.solve()
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("IPM_DEFER", "1")
-    s = ipm355.QPSolver(check_cvxpy=False, suppress_print=True, **kw)
-    for fm in (s.fm, s.phase1_solver.phase1_fm):
-        up, de = fm.prob.kkt_flops()
-        assert de > 0 and up > 0, (up, de)          # the deferral is really exercised
-    v = s.solve()
-    cpu = O.QPSolver(**kw)
-    v_cpu = cpu.solve()
-    assert rel(ref.xstar, cpu.xstar) <= XSTAR_RTOL
-    assert rel(s.xstar, cpu.xstar) <= XSTAR_RTOL, (rel(s.xstar, cpu.xstar), list(s.inner_iters),
-                                                   list(cpu.inner_iters))
-    assert abs(v - v_cpu) <= 1e-8 * max(1.0, abs(v_cpu))
-    del v_ref
-
-
 @pytest.mark.parametrize("method", ["np_solve", "np_lstsq", "direct", "kkt"])
 @pytest.mark.parametrize("name", ["qp_ineq_box", "lp_eq_ineq", "qp_eq_phase1"])
 def test_other_linear_solve_methods(name, method):

@@ -10,7 +10,7 @@
 #include <vector>
 #include "../interiorpoint-gpu_amd/csrc/ipm_blas.hip"
 namespace ipm {
-#include "../interiorpoint-gpu_amd/csrc/ipm_diag2.h"   // lab-only: not part of the library kernel
+#include "ipm_diag2.h"   // lab-only: not part of the library kernel
 }
 
 template <int ROLE>
