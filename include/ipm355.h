@@ -165,6 +165,24 @@ int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v, const ipm_
 int ipm_get_use_backup(ipm_problem* pr);
 int ipm_set_use_backup(ipm_problem* pr, int flag);
 
+/* ---- batched Cholesky across concurrently solved problems (config 4: the reference solves its
+   independent instances one after another, testSolver.py:437-808; here a rank's instances run
+   concurrently, one host thread + stream each, ipm355.dist.Shard).  Problems attached to one
+   batch hand the Cholesky of their Newton steps (NewtonSolver.py:286, 303-313) to it: the
+   factorizations that arrive together (members, or those present when an early arrival's bounded
+   wait runs out) run as ONE launch per 256-column block on the batch's own stream; each result is
+   bitwise that of the problem's own factorization.  Not for problems solved one after another
+   from a single thread (they would only add the wait). */
+typedef struct ipm_potrf_batch ipm_potrf_batch;
+int ipm_potrf_batch_create(int device, ipm_potrf_batch** out);
+int ipm_potrf_batch_destroy(ipm_potrf_batch* b);
+/* delta > 0: that many problems start solving; delta < 0: finished ones leave */
+int ipm_potrf_batch_members(ipm_potrf_batch* b, int delta);
+/* batched launches issued, factorizations they carried (so factorizations / launches = batch size) */
+int ipm_potrf_batch_stats(ipm_potrf_batch* b, double* launches, double* factorizations);
+/* attach (b) or detach (NULL) a problem; b must live on the problem's device */
+int ipm_problem_set_potrf_batch(ipm_problem* pr, ipm_potrf_batch* b);
+
 /* ---- level 1: the oracle protocol (FunctionManager.py:94-195) ---------------- */
 /* update_x(x, update_slacks): the evaluation point becomes x [dev]; slacks are
    recomputed only if update_slacks (Q2) */
@@ -212,8 +230,9 @@ int ipm_getrs(ipm_handle* h, int64_t n, int64_t nrhs, const double* LU, int64_t 
 /* minimum-norm least squares on a symmetric matrix: B <- A^+ B, the np.linalg.lstsq(A, B, rcond=None)
    of the np_lstsq method and of the Cholesky-failure backup (NewtonSolver.py:212-227, 334-341;
    NewtonSolverInfeasibleStart.py:279-316, 692-724).  A full symmetric (column-major, lda), replaced
-   by its eigenvectors; eigenvalues |lambda| <= eps * n * max|lambda| are dropped (gelsd's rcond
-   rule).  B row-major n x nrhs (ldb), in place.  *info: the eigensolver's convergence info (0 = ok,
+   by W = V^T, the TRANSPOSED eigenvector matrix (column-major, lda: column j of A holds row j of V,
+   i.e. A(i, j) = V(j, i), the operand layout of the MFMA apply); eigenvalues
+   |lambda| <= eps * n * max|lambda| are dropped (gelsd's rcond rule).  B row-major n x nrhs (ldb), in place.  *info: the eigensolver's convergence info (0 = ok,
    1 = the hand-written Jacobi eigensolver did not converge) */
 int ipm_lstsq_sym(ipm_handle* h, int64_t n, int64_t nrhs, double* A, int64_t lda, double* B, int64_t ldb,
                   int* info);

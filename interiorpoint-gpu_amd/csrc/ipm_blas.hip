@@ -23,6 +23,7 @@
 #include <tuple>
 #include <vector>
 #include <cstdlib>
+#include <cstring>
 
 namespace ipm {
 
@@ -1197,16 +1198,12 @@ struct RoleTrace {
 // LAZY (default; IPM_LAZYC=0 turns it off.  FASTS launches whose trailing tiles are all whole K = 256 tiles, no strips or
 // K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
 // before the first MFMA
-template <bool VEC, bool FASTS = false, int LAZY = 0>
-__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
-  IPM_KARGS(BlockArgs, b, b_arg);   // (fields loaded where each role uses them: ipm_mfma.h)
-  __shared__ BlockSmem sm;
-  __shared__ int sticket, sflag;
+// The roles of one launch for the workgroup holding launch-local ticket t (see the ticket order
+// below).  Shared by the one-instance kernel (k_potrf_block) and the batched one (k_potrf_batch).
+template <bool VEC, bool FASTS, int LAZY>
+__device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, BlockSmem& sm, int& sflag) {
   const int tid = threadIdx.x;
-  if (tid == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
   unsigned* const failw = &b.ctl[CTL_FAIL];
-  __syncthreads();
-  int64_t t = sticket;
 #ifdef IPM_ROLE_TRACE
   RoleTrace rt(b.trace != 0, (int)t);
 #endif
@@ -1530,6 +1527,50 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
   }
 }
 
+template <bool VEC, bool FASTS = false, int LAZY = 0>
+__global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
+  IPM_KARGS(BlockArgs, b, b_arg);   // (fields loaded where each role uses them: ipm_mfma.h)
+  __shared__ BlockSmem sm;
+  __shared__ int sticket, sflag;
+  if (threadIdx.x == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
+  __syncthreads();
+  potrf_block_body<VEC, FASTS, LAZY>(b, __builtin_amdgcn_readfirstlane(sticket), sm, sflag);
+}
+
+// ---- batched launches (config 4: several instances' factorizations in lockstep).  One launch
+// covers block column bk of every instance in the batch group: tab[i] is instance i's BlockArgs
+// (exactly what its own k_potrf_block launch would take), and the workgroups draw ONE ticket
+// sequence ordered role class by role class -- every instance's look-ahead tiles, then every
+// P(a) diagonal role, the critical row chunks, fold tiles, P(b) diagonal roles, ragged rows,
+// trailing tiles, the other row chunks -- so that each instance's critical chain starts as early
+// as in its own launch.  Inside an instance the launch-local tickets keep their order (a
+// workgroup still waits only for lower tickets of its own instance: no deadlock for any
+// residency), and every instance runs its own plan: results are bitwise those of its own launch.
+// dec: [0, K) global start of (class c, instance i) at c * B + i (non-decreasing), [K, 2K) the
+// launch-local ticket of that class's first item; K = POTRF_NCLS * B.
+constexpr int POTRF_NCLS = 9;
+template <bool VEC, bool FASTS = false, int LAZY = 0>
+__global__ __launch_bounds__(256, 2) void k_potrf_batch(const BlockArgs* __restrict__ tab, const int* __restrict__ dec,
+                                                        int B, unsigned* gticket) {
+  __shared__ BlockSmem sm;
+  __shared__ int sticket, sflag;
+  if (threadIdx.x == 0) sticket = (int)atomicAdd(gticket, 1u);
+  __syncthreads();
+  const int T = __builtin_amdgcn_readfirstlane(sticket);
+  // the last class/instance entry whose global start is <= T (empty entries repeat the next start)
+  const int K = POTRF_NCLS * B;
+  int lo = 0, hi = K - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (dec[mid] <= T) lo = mid;
+    else hi = mid - 1;
+  }
+  const int k = __builtin_amdgcn_readfirstlane(lo);
+  const int i = k % B;
+  const int64_t t = (int64_t)dec[K + k] + (T - dec[k]);
+  potrf_block_body<VEC, FASTS, LAZY>(tab[i], t, sm, sflag);
+}
+
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
 static constexpr int64_t PANEL_WS = PF_DINV + 36 * 256;
 
@@ -1668,23 +1709,38 @@ static unsigned long long wall_ticks(unsigned us) {
   return t > 0 ? t : 1;
 }
 constexpr unsigned SPIN_US_DEFAULT = 1000000;   // 1 s: no legitimate wait comes near it
-// (the device global ipm_spin_ticks of the current device; its initial value is 1 s at 100 MHz)
+// (the device global ipm_spin_ticks, initially 1 s at 100 MHz, on EVERY visible device: a process
+// may drive several GPUs.  Every kernel that spins -- the Cholesky, the split / stream-K tiles, the
+// backward solve -- is launched from this translation unit, so this TU's copy of the header's
+// static global is the one they read.)
 static void set_spin_ticks(int which, unsigned us) {
   const unsigned long long t = wall_ticks(us ? us : SPIN_US_DEFAULT);
-  hipMemcpyToSymbol(HIP_SYMBOL(ipm_spin_ticks), &t, sizeof(t), which * sizeof(t), hipMemcpyHostToDevice);
+  int cur = 0, cnt = 0;
+  hipGetDevice(&cur);
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt < 1) cnt = 1;
+  for (int d = 0; d < cnt; ++d) {
+    if (hipSetDevice(d) != hipSuccess) continue;
+    hipMemcpyToSymbol(HIP_SYMBOL(ipm_spin_ticks), &t, sizeof(t), which * sizeof(t), hipMemcpyHostToDevice);
+  }
+  hipSetDevice(cur);
 }
 void set_potrf_spin_limit_us(unsigned us) { set_spin_ticks(0, us); }
 
-void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
-  if (ncols < 0 || ncols > n) ncols = n;
-  if (ncols <= 0) {
-    hipMemsetAsync(info, 0, sizeof(int), st);
-    return;
-  }
+// One planned launch of the factorization: its arguments, grid and kernel instantiation
+// (0 <true,true,1> lazy-C, 1 <true,true,2> pair lazy-C, 2 <true,true> fast loop, 3 <true,false>,
+// 4 <false,false>), and the sizes of its ticket classes in ticket order (k_potrf_batch).
+struct BlockLaunch {
+  BlockArgs b;
+  int64_t grid = 0;
+  int inst = 4;
+  int64_t cls[POTRF_NCLS] = {};
+};
+// every launch of one factorization (potrf_lower_fused's plan); the control words are NOT zeroed
+static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
+                       std::vector<BlockLaunch>& out) {
+  out.clear();
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
-  // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
-  zero2(st, info, 1, ctl0, 8 + nblocks * cw);
   const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
   // IPM_RAG=0: ragged trailing rows as a row of 128-tiles (read per call: tests compare both)
   const char* erag = getenv("IPM_RAG");
@@ -1912,7 +1968,8 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
       b.sscr = ws + potrf_split_scratch_off(n);
       b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
     }
-    const int64_t grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns;
+    BlockLaunch L;
+    L.grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
@@ -1920,12 +1977,152 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     const bool lazy = lazy_on && fasts && b.s.K == CH_NB && b.nstrip == 0 && b.s_full == b.ns;
     const bool lazy2 = lazy2_on && fasts && b.s.K == 2 * CH_NB && b.nstrip + b.s_full == b.ns &&
                        (b.nstrip == 0 || b.s2.K == 2 * CH_NB) && (b.nrag == 0 || b.rag_K <= 2 * CH_NB);
-    if (vec && lazy) hipLaunchKernelGGL((k_potrf_block<true, true, 1>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (vec && lazy2) hipLaunchKernelGGL((k_potrf_block<true, true, 2>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (vec && fasts) hipLaunchKernelGGL((k_potrf_block<true, true>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else if (vec) hipLaunchKernelGGL((k_potrf_block<true, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((k_potrf_block<false, false>), dim3((unsigned)grid), dim3(256), 0, st, b);
+    L.inst = (vec && lazy) ? 0 : (vec && lazy2) ? 1 : (vec && fasts) ? 2 : vec ? 3 : 4;
+    // ticket classes in launch-local order (potrf_block_body's decode)
+    const int64_t nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
+    const int64_t cls[POTRF_NCLS] = {b.nla, 1, nchd, b.nnf, b.wbw > 0 ? 1 : 0, b.nrag, b.ns, b.nra - nchd, b.nrb};
+    for (int c = 0; c < POTRF_NCLS; ++c) L.cls[c] = cls[c];
+    L.b = b;
+    out.push_back(L);
   }
+}
+
+static void launch_block(hipStream_t st, const BlockLaunch& L) {
+  const dim3 g((unsigned)L.grid), t(256);
+  switch (L.inst) {
+    case 0: hipLaunchKernelGGL((k_potrf_block<true, true, 1>), g, t, 0, st, L.b); break;
+    case 1: hipLaunchKernelGGL((k_potrf_block<true, true, 2>), g, t, 0, st, L.b); break;
+    case 2: hipLaunchKernelGGL((k_potrf_block<true, true>), g, t, 0, st, L.b); break;
+    case 3: hipLaunchKernelGGL((k_potrf_block<true, false>), g, t, 0, st, L.b); break;
+    default: hipLaunchKernelGGL((k_potrf_block<false, false>), g, t, 0, st, L.b); break;
+  }
+}
+
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
+  if (ncols < 0 || ncols > n) ncols = n;
+  if (ncols <= 0) {
+    hipMemsetAsync(info, 0, sizeof(int), st);
+    return;
+  }
+  thread_local std::vector<BlockLaunch> plan;
+  potrf_plan(n, A, lda, info, ws, ncols, plan);
+  // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
+  unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
+  zero2(st, info, 1, ctl0, 8 + (int64_t)plan.size() * block_ctl_words(n));
+  for (const BlockLaunch& L : plan) launch_block(st, L);
+}
+
+// ---- batched factorizations (k_potrf_batch).  Argument tables in device memory, one copy per call
+// from pinned staging: [zero list (B)][ticket counters (launch groups)][per group: BlockArgs x Bg,
+// dec ints x 2 K].  Every instance keeps its own plan, control words and workspace.
+struct ZeroEnt {
+  unsigned* ctl0;
+  int64_t words;
+  int* info;
+};
+__global__ void k_zero_batch(const ZeroEnt* __restrict__ ents, int B, unsigned* counters, int ng) {
+  if ((int)blockIdx.x < B) {
+    const ZeroEnt e = ents[blockIdx.x];
+    for (int64_t i = threadIdx.x; i < e.words; i += blockDim.x) e.ctl0[i] = 0u;
+    if (threadIdx.x == 0 && e.info) *e.info = 0;
+  } else {
+    for (int i = threadIdx.x; i < ng; i += blockDim.x) counters[i] = 0u;
+  }
+}
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int potrf_lower_batch(hipStream_t st, const PotrfReq* reqs, int B, PotrfBatchWs& w) {
+  if (B <= 0) return 0;
+  thread_local std::vector<std::vector<BlockLaunch>> plans;
+  plans.resize(B);
+  size_t maxl = 0;
+  for (int i = 0; i < B; ++i) {
+    const PotrfReq& r = reqs[i];
+    const int64_t nc = (r.ncols < 0 || r.ncols > r.n) ? r.n : r.ncols;
+    if (nc > 0) potrf_plan(r.n, r.A, r.lda, r.info, r.ws, nc, plans[i]);
+    else plans[i].clear();
+    maxl = std::max(maxl, plans[i].size());
+  }
+  // launch groups: block column bk of every instance that has one, split by kernel instantiation
+  struct Group { size_t bk; int inst; std::vector<int> ids; size_t tab_off, dec_off; int64_t grid; };
+  std::vector<Group> groups;
+  for (size_t bk = 0; bk < maxl; ++bk)
+    for (int inst = 0; inst < 5; ++inst) {
+      Group g{bk, inst, {}, 0, 0, 0};
+      for (int i = 0; i < B; ++i)
+        if (plans[i].size() > bk && plans[i][bk].inst == inst) g.ids.push_back(i);
+      if (!g.ids.empty()) groups.push_back(std::move(g));
+    }
+  const int ng = (int)groups.size();
+  size_t off = align_up(sizeof(ZeroEnt) * B, 256);
+  const size_t cnt_off = off;
+  off = align_up(off + sizeof(unsigned) * std::max(ng, 1), 256);
+  for (Group& g : groups) {
+    g.tab_off = off;
+    off = align_up(off + sizeof(BlockArgs) * g.ids.size(), 256);
+    g.dec_off = off;
+    off = align_up(off + sizeof(int) * 2 * POTRF_NCLS * g.ids.size(), 256);
+  }
+  const size_t need = off;
+  if (need > w.bytes) {
+    hipStreamSynchronize(st);   // (the old tables may still be read by queued launches)
+    if (w.dev) hipFree(w.dev);
+    if (w.host) hipHostFree(w.host);
+    w.dev = w.host = nullptr;
+    w.bytes = 0;
+    const size_t sz = std::max<size_t>(need * 2, 1 << 16);
+    if (hipMalloc(&w.dev, sz) != hipSuccess || hipHostMalloc(&w.host, sz) != hipSuccess) return -1;
+    w.bytes = sz;
+  }
+  if (!w.copied) hipEventCreateWithFlags(&w.copied, hipEventDisableTiming);
+  else hipEventSynchronize(w.copied);   // the staging buffer's previous copy has landed
+  char* h = static_cast<char*>(w.host);
+  char* d = static_cast<char*>(w.dev);
+  ZeroEnt* ze = reinterpret_cast<ZeroEnt*>(h);
+  for (int i = 0; i < B; ++i) {
+    ze[i].ctl0 = reinterpret_cast<unsigned*>(reqs[i].ws + 2 * PANEL_WS);
+    ze[i].words = plans[i].empty() ? 0 : 8 + (int64_t)plans[i].size() * block_ctl_words(reqs[i].n);
+    ze[i].info = reqs[i].info;
+  }
+  for (Group& g : groups) {
+    const int Bg = (int)g.ids.size(), K = POTRF_NCLS * Bg;
+    BlockArgs* tab = reinterpret_cast<BlockArgs*>(h + g.tab_off);
+    int* dec = reinterpret_cast<int*>(h + g.dec_off);
+    int64_t gstart = 0;
+    for (int j = 0; j < Bg; ++j) std::memcpy(static_cast<void*>(&tab[j]), &plans[g.ids[j]][g.bk].b, sizeof(BlockArgs));
+    for (int c = 0; c < POTRF_NCLS; ++c)
+      for (int j = 0; j < Bg; ++j) {
+        const BlockLaunch& L = plans[g.ids[j]][g.bk];
+        int64_t lstart = 0;
+        for (int c2 = 0; c2 < c; ++c2) lstart += L.cls[c2];
+        dec[c * Bg + j] = (int)gstart;
+        dec[K + c * Bg + j] = (int)lstart;
+        gstart += L.cls[c];
+      }
+    g.grid = gstart;
+  }
+  if (hipMemcpyAsync(w.dev, w.host, need, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+  hipEventRecord(w.copied, st);
+  unsigned* counters = reinterpret_cast<unsigned*>(d + cnt_off);
+  hipLaunchKernelGGL(k_zero_batch, dim3((unsigned)B + 1), dim3(256), 0, st, reinterpret_cast<const ZeroEnt*>(d), B,
+                     counters, ng);
+  for (int q = 0; q < ng; ++q) {
+    const Group& g = groups[q];
+    if (g.grid <= 0) continue;
+    const BlockArgs* tab = reinterpret_cast<const BlockArgs*>(d + g.tab_off);
+    const int* dec = reinterpret_cast<const int*>(d + g.dec_off);
+    const dim3 gr((unsigned)g.grid), t(256);
+    const int Bg = (int)g.ids.size();
+    switch (g.inst) {
+      case 0: hipLaunchKernelGGL((k_potrf_batch<true, true, 1>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
+      case 1: hipLaunchKernelGGL((k_potrf_batch<true, true, 2>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
+      case 2: hipLaunchKernelGGL((k_potrf_batch<true, true>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
+      case 3: hipLaunchKernelGGL((k_potrf_batch<true, false>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
+      default: hipLaunchKernelGGL((k_potrf_batch<false, false>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
+    }
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 static int num_cus() {

@@ -95,6 +95,8 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 // stops waiting (it sees failw).  The host turns a negative info into IPM_HIP_ERROR: the factor is
 // never used.  The bounds live in a device global read only on the slow path (after 16 polls), so
 // the waits hold no extra registers in the kernels around them.  [0]: Cholesky, [1]: backward solve.
+// (A static global in a header: each translation unit has its own copy.  The kernels that spin are
+// all launched from ipm_blas.hip, whose copy set_spin_ticks updates on every device.)
 static __device__ unsigned long long ipm_spin_ticks[2] = {100000000ull, 100000000ull};   // 1 s
 __device__ __forceinline__ void spin_fail(int* info, unsigned* failw) {
   if (info) atomicCAS(info, 0, POTRF_INFO_SPIN);

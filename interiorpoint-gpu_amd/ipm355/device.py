@@ -222,6 +222,12 @@ class DeviceProblem:
                 "k_gemv_t_part (gradient: C^T w)": (ms[1], 8.0 * (m * n + m + n)),
                 "k_ls_lin (64 line-search candidates)": (ms[2], 16.0 * S)}
 
+    def set_potrf_batch(self, batch):
+        """Hand this problem's Newton-step Cholesky to a PotrfBatch (None: back to its own stream).
+        The batch must stay alive while the problem uses it."""
+        self._potrf_batch = batch
+        self.check(self.handle.lib.ipm_problem_set_potrf_batch(self.ptr, batch.ptr if batch is not None else None))
+
     @property
     def use_backup(self):
         return bool(self.handle.lib.ipm_get_use_backup(self.ptr))

@@ -93,16 +93,22 @@ class Shard:
 
     concurrent=True (config 4): every instance gets its own HIP stream -- its solver and native
     handle are created under ``torch.cuda.stream(stream)`` -- and ``solve()`` runs the instances
-    from one host thread each (the native calls release the GIL), so their kernels overlap on the
-    GPU.  The HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default;
+    from one host thread per distinct stream (the native calls release the GIL), so their kernels
+    overlap on the GPU.  The HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default;
     streams sharing a queue serialise): call ``configure_queues()`` before anything initialises
     the GPU.  concurrent=False: one after another on the current stream."""
 
-    def __init__(self, make_instance, indices, solver_cls, kwargs=None, device=None, concurrent=False):
+    def __init__(self, make_instance, indices, solver_cls, kwargs=None, device=None, concurrent=False,
+                 batch=None):
         import torch
         self.indices = list(indices)
         self.dev = local_device(device)
         self.concurrent = bool(concurrent)
+        # batched Cholesky (ipm_potrf_batch): the concurrent instances' factorizations run as one
+        # launch per 256-column block (default with concurrent=True; IPM_POTRF_BATCH=0 turns it off)
+        if batch is None:
+            batch = self.concurrent and os.environ.get("IPM_POTRF_BATCH", "1") != "0"
+        self.batch = None
         self.streams = ([torch.cuda.Stream(device=torch.device("cuda", self.dev)) for _ in self.indices]
                         if self.concurrent else [None] * len(self.indices))
         self.solvers = []
@@ -113,6 +119,12 @@ class Shard:
             if s.dev.index != self.dev:
                 raise RuntimeError(f"solver placed on {s.dev}, rank owns cuda:{self.dev}")
             self.solvers.append(s)
+        if batch and self.concurrent and len(self.solvers) > 1:
+            from ._lib import PotrfBatch
+            self.batch = PotrfBatch(self.dev)
+            for s in self.solvers:
+                for prob in _device_problems(s):
+                    prob.set_potrf_batch(self.batch)
 
     def solve(self, **solve_kwargs):
         """Solve every instance (solve_kwargs go to each solver's solve(), e.g. iteration_budget);
@@ -130,9 +142,26 @@ class Shard:
             iters = int(sum(s.inner_iters)) + (int(sum(p1.inner_iters)) if p1 is not None else 0)
             return self.indices[k], (value, iters, time.perf_counter() - t0)
         if self.concurrent and len(self.solvers) > 1:
+            # one host thread per DISTINCT stream: torch hands out streams from a pool of 32 per
+            # device, so past 32 instances (or beside another Shard) two instances can share a
+            # stream -- and with it the native handle (Handle.get caches one per (device, stream)),
+            # whose staging buffers and scratch are not safe to drive from two threads.  Instances
+            # sharing a stream run one after another in that stream's thread.
             from concurrent.futures import ThreadPoolExecutor
-            with ThreadPoolExecutor(max_workers=len(self.solvers)) as ex:
-                out = dict(ex.map(one, range(len(self.solvers))))
+            groups = {}
+            for k, st in enumerate(self.streams):
+                groups.setdefault(st.cuda_stream, []).append(k)
+
+            def run_group(ks):
+                try:
+                    return [one(k) for k in ks]
+                finally:
+                    if self.batch is not None:
+                        self.batch.members(-1)      # this thread solves no more: stop waiting for it
+            if self.batch is not None:
+                self.batch.members(len(groups))
+            with ThreadPoolExecutor(max_workers=len(groups)) as ex:
+                out = dict(r for rs in ex.map(run_group, list(groups.values())) for r in rs)
         else:
             out = dict(one(k) for k in range(len(self.solvers)))
         if torch.cuda.is_available():
@@ -141,6 +170,20 @@ class Shard:
 
     def xstar(self):
         return {i: s.xstar for i, s in zip(self.indices, self.solvers)}
+
+
+def _device_problems(solver):
+    """The DeviceProblems a solver's Newton steps run on: its barrier problem and, when it has one,
+    its phase-1 problem."""
+    out = []
+    fm = getattr(solver, "fm", None)
+    if fm is not None and getattr(fm, "prob", None) is not None:
+        out.append(fm.prob)
+    p1 = getattr(solver, "phase1_solver", None)
+    fm1 = getattr(p1, "phase1_fm", None) if p1 is not None else None
+    if fm1 is not None and getattr(fm1, "prob", None) is not None:
+        out.append(fm1.prob)
+    return out
 
 
 def _on(stream):

@@ -125,3 +125,46 @@ def test_shard_solves_every_instance_once_with_solve_kwargs(monkeypatch):
     assert calls == [{"iteration_budget": 7}] * 3
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")     # (restored after the test)
     assert D.configure_queues(16) in (True, False)
+
+
+def test_shard_concurrent_groups_instances_by_stream():
+    """with more instances than torch's pool of 32 streams per device, two instances
+    share a stream and hence a native handle (Handle.get caches one per (device, stream)).
+    Shard.solve must never drive one stream from two host threads at once: instances sharing a
+    stream run one after another in that stream's thread (host logic only: fake streams and
+    solvers that fail if two threads enter the same stream)."""
+    import threading
+    import time
+    from ipm355 import dist as D
+
+    class FakeStream:
+        def __init__(self, sid):
+            self.cuda_stream = sid
+
+        def synchronize(self):
+            pass
+
+    active, lock, seen = {}, threading.Lock(), set()
+
+    class FakeSolver:
+        def __init__(self, sid):
+            self.sid, self.inner_iters = sid, [3]
+
+        def solve(self):
+            with lock:
+                assert not active.get(self.sid), "two threads drive one stream"
+                active[self.sid] = True
+                seen.add(threading.get_ident())
+            time.sleep(0.005)
+            with lock:
+                active[self.sid] = False
+            return float(self.sid)
+
+    sh = object.__new__(D.Shard)
+    sh.indices, sh.dev, sh.concurrent, sh.batch = list(range(40)), 0, True, None
+    sh.streams = [FakeStream(i % 32) for i in range(40)]
+    sh.solvers = [FakeSolver(i % 32) for i in range(40)]
+    out = sh.solve()
+    assert sorted(out) == list(range(40))
+    assert all(out[i][0] == float(i % 32) and out[i][1] == 3 for i in range(40))
+    assert len(seen) > 1          # still concurrent across distinct streams

@@ -351,6 +351,33 @@ def test_newton_step_discarded_when_cholesky_wait_runs_out():
     assert rel(s.xstar, c.xstar) <= XSTAR_RTOL
 
 
+def test_lstsq_failure_feasible_start_first_iteration():
+    """the feasible-start linalg-error path (NewtonSolver.py:148-155).  An eigensolve that
+    does not converge at the FIRST Newton iteration: the reference's except branch returns ``nd``,
+    which is still unbound there, so the reference raises UnboundLocalError out of solve(); the
+    device path deliberately ends that Newton solve as an ordinary failure instead (1 iteration,
+    success False, x unchanged -- DESIGN.md §2.1).  np_lstsq LP with phase 1 (the phase-1 solver
+    uses the same linear_solve_method): force the first eigensolve to fail."""
+    import ipm355
+    from ipm355 import _lib as L
+    z = load("meth_lp_ineq_box_np_lstsq")
+    kw = solver_kwargs(z)
+    kw["x0"] = z["x_init"].copy()
+    h = L.Handle.get(0)
+    s = ipm355.LPSolver(check_cvxpy=False, suppress_print=True, **kw)
+    try:
+        h.lib.ipm_debug_lstsq_fail_call(0)
+        s.solve()
+    finally:
+        h.lib.ipm_debug_lstsq_fail_call(-1)
+    p1 = s.phase1_solver
+    assert p1 is not None and int(p1.inner_iters[0]) == 1, list(p1.inner_iters)
+    assert int(z["phase1_inner_iters"][0]) > 1
+    # and without the knob the run is the reference's again
+    z2, s2, v2 = _run("meth_lp_ineq_box_np_lstsq")
+    assert list(s2.inner_iters) == list(z2["inner_iters"])
+
+
 def test_lstsq_failure_is_sticky_across_eigensolves():
     """the np_lstsq block elimination runs two eigensolves per Newton step (H,
     then S = A H^+ A^T) into one status word.  Force the FIRST to report non-convergence (debug

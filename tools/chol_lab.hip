@@ -98,12 +98,10 @@ int main(int argc, char** argv) {
     printf("%-44s median %7.0f cycles  min %7.0f  | event median %6.1f us | info %d | max|L-host|/max|L| %.1e  max|L-L_v0| %.1e\n",
            name, cy[cy.size() / 2], cy[0], us[us.size() / 2], inf, dref / nrm, d0);
   };
-  run(k_lab_diag<0>, "V0 current");
-  run(k_lab_diag<1>, "V1 deferred store wait");
-  run(k_lab_diag<2>, "V2 branch-free LDS loads/stores");
-  run(k_lab_diag<3>, "V3 = V1 + V2");
-  run(k_lab_diag<130>, "V130 = V2 + no look-ahead tiles on wave 3");
-  run(k_lab_diag<131>, "V131 = V130 + deferred store wait");
-  run(k_lab_diag<0>, "V0 current (again)");
+  run(k_lab_diag<130>, "V130 shipped (IPM_DIAG_V)");
+  run(k_lab_diag<130 + 32768>, "V130 + ONE register stream (readlane multipliers)");
+  run(k_lab_diag<130 + 16>, "V130 + builtin DPP broadcast shared by both streams");
+  run(k_lab_diag<130 + 64>, "V130 + tile rows through readlane multipliers");
+  run(k_lab_diag<130>, "V130 shipped (again)");
   return 0;
 }
