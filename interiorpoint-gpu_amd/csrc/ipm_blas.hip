@@ -1221,7 +1221,17 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   // look-ahead tiles: the first 128 rows x 128 columns (what the P(a) diagonal role waits for,
   // lower part only) as 32 x 32 tiles -- ten short tiles instead of three 64-tiles on the chain --
   // then 64-tiles for rows >= 128.  la_done[64-row block] counts finished tiles of that block.
-  if (t < b.nla) {
+  // fold tiles (K_NF below): the look-ahead 32-tiles of the P(a) diagonal block -- what its
+  // diagonal role waits for, on the chain -- and the tiles folding P(a) into P(b)'s diagonal block
+  // run ONE code path: every operand of a K = 128 pass staged in LDS by 16-byte direct loads, then
+  // a register MFMA chain (a second inlined copy of it cost the r4w kernel its register allocation)
+  int64_t fo = 0, fsrc = 0;            // destination block origin (rows = columns), first source column
+  int fni = 0, fnj = 0, fnp = 0;       // destination rows / columns (<= 128), K passes of 128 columns
+  int ftile = 0, frole = 9;            // tile in the lower-triangle enumeration, trace role
+  unsigned* fdone = nullptr;           // completion counter
+  bool fwait = false;                  // wait for P(a)'s published rows of P(b)'s diagonal block
+  const bool la_fold = VEC && t < b.nla32 && (b.la32.K % 128) == 0;
+  if (t < b.nla && !la_fold) {
     ROLE(0);
     int64_t rb;
     if (t < b.nla32) {
@@ -1248,6 +1258,19 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&la_done[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
+  }
+  if (la_fold) {
+    int64_t i = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);   // tri row of tile t
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    while (i * (i + 1) / 2 > t) --i;
+    fo = b.cb;
+    fni = (int)b.la32.ni;
+    fnj = (int)b.la32.nj;
+    fsrc = b.cb - b.la32.K;
+    fnp = (int)(b.la32.K / 128);
+    ftile = (int)t;
+    frole = 0;
+    fdone = &la_done[i >> 1];
   }
   t -= b.nla;
   // LA row blocks [r0/64, r1/64] (rows relative to cb) finished
@@ -1278,13 +1301,22 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   enum { K_DIAG, K_ROW, K_NF, K_TILE, K_RAG, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
-  if (t == 0) {
+  if (la_fold) {
+    kind = K_NF;
+  } else if (t == 0) {
     kind = K_DIAG;
   } else if ((t -= 1) < nchd) {
     kind = K_ROW;
     chunk = t;
   } else if ((t -= nchd) < b.nnf) {
     kind = K_NF;
+    fo = k1;
+    fni = fnj = b.wbw;
+    fsrc = b.cb;
+    fnp = 1;
+    ftile = (int)t;
+    fdone = &b.ctl[CTL_NF];
+    fwait = true;
   } else {
     t -= b.nnf;
     if (b.wbw > 0 && t == 0) {
@@ -1311,7 +1343,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   int crit = -1;
   if (kind == K_DIAG) crit = pb ? NCRIT - 1 : 0;
   else if (kind == K_ROW && !pb && chunk < nchd) crit = 1 + (int)chunk;
-  else if (kind == K_NF) crit = 1 + nchd + (int)t;
+  else if (kind == K_NF && fwait) crit = 1 + nchd + (int)t;
   if (crit >= NCRIT - 1 && !(kind == K_DIAG && pb)) crit = -1;   // (table full: not tracked)
   if (crit >= 0 && tid == 0)
     __hip_atomic_store(&b.ctl[CTL_CRIT + crit], 1u + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1350,85 +1382,94 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     return;
   }
   if (kind == K_NF) {
-    ROLE(9);
-    // P(b)'s diagonal block -= L1D L1D^T, L1D = P(a)'s rows of that block (published by the first
-    // nchd row chunks): one 32 x 32 lower tile per workgroup, 16 x 16 per wave, K = wa = 128
-    int T = (b.wbw + 31) / 32, ti = 0, q = (int)t;
-    while (q > ti) { q -= ti + 1; ++ti; }   // t -> (ti, tj = q), tj <= ti
+    ROLE(frole);
+    // destination block D (rows / columns fo.., fni x fnj, lower) -= L L^T over the fnp source
+    // column passes [fsrc + 128 p, fsrc + 128 p + 128): one 32 x 32 lower tile per workgroup,
+    // 16 x 16 per wave.  NF: D = P(b)'s diagonal block, L = P(a)'s rows of it (published by the
+    // first nchd row chunks, fwait).  Look-ahead: D = P(a)'s diagonal block, L = the previous
+    // block's (or pair's) columns of its rows, final since the previous launch.
+    int ti = 0, q = ftile;
+    while (q > ti) { q -= ti + 1; ++ti; }   // ftile -> (ti, tj = q), tj <= ti
     const int tj = q;
-    (void)T;
-    if (tid == 0)
-      spin_until<2>(b.info, failw, [&] {
-        return ld_ctl(&b.ctl[CTL_PA_NEXT]) >= (unsigned)nchd || ld_ctl(&b.ctl[CTL_PA_PROG]) == 0xFFFFFFFFu;
-      });
-    __syncthreads();
+    if (fwait) {
+      if (tid == 0)
+        spin_until<2>(b.info, failw, [&] {
+          return ld_ctl(&b.ctl[CTL_PA_NEXT]) >= (unsigned)nchd || ld_ctl(&b.ctl[CTL_PA_PROG]) == 0xFFFFFFFFu;
+        });
+      __syncthreads();
+    }
     ROLE_STAMP(wake);
     const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, fk = lane >> 4;
     const int ib = 32 * ti + 16 * (wv & 1), jb = 32 * tj + 16 * (wv >> 1);
     const bool live = ib + 15 >= jb;   // sub-tiles entirely above the diagonal are never read
     const int i = ib + fr;
-    const bool iin = i < b.wbw, jin = jb + fr < b.wbw;
+    const bool iin = i < fni, jin = jb + fr < fnj;
+    double* const D = b.A + fo * b.lda + fo;   // D(i, j) at D[j * lda + i]
     dbl4 acc;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = jb + fk + 4 * r;
-      acc[r] = (live && iin && j < b.wbw) ? ld_sc1(&b.A[(k1 + j) * b.lda + k1 + i]) : 0.0;
+      acc[r] = (live && iin && j < fnj) ? ld_sc1(&D[j * b.lda + i]) : 0.0;
     }
     if constexpr (VEC) {
-      // the two 32-row blocks of L1D (rows 32 tj.. for the A operand, 32 ti.. for B; all 128
-      // columns) go to LDS with 16-byte direct loads: one wave instruction = 4 columns x 32 rows
-      // (lane l: rows 2 (l & 15), +1 of column l >> 4), element (c, r) of block s at
+      // per pass, the two 32-row blocks of L (rows 32 tj.. for the A operand, 32 ti.. for B; the
+      // pass's 128 columns) go to LDS with 16-byte direct loads: one wave instruction = 4 columns x
+      // 32 rows (lane l: rows 2 (l & 15), +1 of column l >> 4), element (c, r) of block s at
       // sL[4096 s + 32 c + r].  16 instructions per wave instead of 64 8-byte strided loads, which
       // ran past the 63 outstanding loads a wave may hold (r4u trace: 10.7 us from the wake to the
-      // operands, 2-3 us for the diagonal role's 128 KB panel the same way).  Rows past wbw read
-      // the next rows / column of the matrix (in bounds: P(b)'s columns follow) and are masked.
+      // operands).  Rows past fni read the next rows / column of the matrix (in bounds) and are
+      // masked.
       double* sL = sm.d.sD;
       const int nsrc = ti == tj ? 1 : 2;
-      for (int it = wv; it < 32 * nsrc; it += 4) {
-        const int sblk = it >> 5, c4 = it & 31;
-        const int col = 4 * c4 + (lane >> 4);
-        const double* src = b.A + (b.cb + col) * b.lda + k1 + 32 * (sblk ? ti : tj) + 2 * (lane & 15);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)&sL[sblk * 4096 + c4 * 128], 16, 0,
-                                         16);   // aux 16 = sc1
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      ROLE_STAMP(loaded);
-      if (live) {
-        const double* sa = sL + 16 * (wv >> 1) + fr;                          // L1D[jb + fr][k] at sa[32 k]
-        const double* sbp = sL + (ti == tj ? 0 : 4096) + 16 * (wv & 1) + fr;   // L1D[i][k]
+      for (int p = 0; p < fnp; ++p) {
+        if (p) __syncthreads();   // (the previous pass's operands are consumed)
+        for (int it = wv; it < 32 * nsrc; it += 4) {
+          const int sblk = it >> 5, c4 = it & 31;
+          const int col = 128 * p + 4 * c4 + (lane >> 4);
+          const double* src = b.A + (fsrc + col) * b.lda + fo + 32 * (sblk ? ti : tj) + 2 * (lane & 15);
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)&sL[sblk * 4096 + c4 * 128], 16,
+                                           0, 16);   // aux 16 = sc1
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        ROLE_STAMP(loaded);
+        if (live) {
+          const double* sa = sL + 16 * (wv >> 1) + fr;                          // L[jb + fr][k] at sa[32 k]
+          const double* sbp = sL + (ti == tj ? 0 : 4096) + 16 * (wv & 1) + fr;   // L[i][k]
 #pragma unroll
-        for (int q = 0; q < 32; ++q) {
-          const int k = 4 * q + fk;
-          const double av = jin ? -sa[32 * k] : 0.0, bv = iin ? sbp[32 * k] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          for (int qq = 0; qq < 32; ++qq) {
+            const int k = 4 * qq + fk;
+            const double av = jin ? -sa[32 * k] : 0.0, bv = iin ? sbp[32 * k] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          }
         }
       }
     } else if (live) {
-      const double* pa = b.A + b.cb * b.lda + k1 + jb + fr;   // L1D[jb + fr][k] at pa[k * lda]
-      const double* pbp = b.A + b.cb * b.lda + k1 + i;        // L1D[i][k]
+      // (NF only: unaligned operands never take the look-ahead path above)
+      const double* pa = b.A + fsrc * b.lda + fo + jb + fr;   // L[jb + fr][k] at pa[k * lda]
+      const double* pbp = b.A + fsrc * b.lda + fo + i;        // L[i][k]
       // all 64 operand loads in flight at once (one latency, not eight)
       double av[32], bv[32];
 #pragma unroll
-      for (int q = 0; q < 32; ++q) {
-        const int64_t k = 4 * q + fk;
-        av[q] = jin ? -ld_sc1(pa + k * b.lda) : 0.0;
-        bv[q] = iin ? ld_sc1(pbp + k * b.lda) : 0.0;
+      for (int qq = 0; qq < 32; ++qq) {
+        const int64_t k = 4 * qq + fk;
+        av[qq] = jin ? -ld_sc1(pa + k * b.lda) : 0.0;
+        bv[qq] = iin ? ld_sc1(pbp + k * b.lda) : 0.0;
       }
 #pragma unroll
-      for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q], bv[q], acc, 0, 0, 0);
+      for (int qq = 0; qq < 32; ++qq) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[qq], bv[qq], acc, 0, 0, 0);
     }
     if (live && iin) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = jb + fk + 4 * r;
-        if (j < b.wbw) st_sc1(&b.A[(k1 + j) * b.lda + k1 + i], acc[r]);
+        if (j < fnj) st_sc1(&D[j * b.lda + i], acc[r]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&b.ctl[CTL_NF], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(fdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if (kind == K_RAG) {

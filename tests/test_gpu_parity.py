@@ -356,8 +356,8 @@ def test_lstsq_failure_feasible_start_first_iteration():
     does not converge at the FIRST Newton iteration: the reference's except branch returns ``nd``,
     which is still unbound there, so the reference raises UnboundLocalError out of solve(); the
     device path deliberately ends that Newton solve as an ordinary failure instead (1 iteration,
-    success False, x unchanged -- DESIGN.md §2.1).  np_lstsq LP with phase 1 (the phase-1 solver
-    uses the same linear_solve_method): force the first eigensolve to fail."""
+    success False, x unchanged -- DESIGN.md §2.1).  np_lstsq LP with phase 1 (on the Cholesky
+    path): force the first eigensolve -- the first centering step's first Newton step -- to fail."""
     import ipm355
     from ipm355 import _lib as L
     z = load("meth_lp_ineq_box_np_lstsq")
@@ -370,9 +370,9 @@ def test_lstsq_failure_feasible_start_first_iteration():
         s.solve()
     finally:
         h.lib.ipm_debug_lstsq_fail_call(-1)
-    p1 = s.phase1_solver
-    assert p1 is not None and int(p1.inner_iters[0]) == 1, list(p1.inner_iters)
-    assert int(z["phase1_inner_iters"][0]) > 1
+    # (phase 1 runs on the Cholesky path: the first eigensolve is the first centering step's)
+    assert int(s.inner_iters[0]) == 1, list(s.inner_iters)
+    assert int(z["inner_iters"][0]) > 1
     # and without the knob the run is the reference's again
     z2, s2, v2 = _run("meth_lp_ineq_box_np_lstsq")
     assert list(s2.inner_iters) == list(z2["inner_iters"])

@@ -293,10 +293,7 @@ int main() {
   }
   };
   stamped(k_stamped<130>, 130);
-  stamped(k_stamped<130 + 256>, 130 + 256);
-  stamped(k_stamped<2 + 256>, 2 + 256);
-  stamped(k_stamped<131>, 131);
-  stamped(k_stamped<130 + 512>, 130 + 512);
+  stamped(k_stamped<130 + 8192>, 130 + 8192);
 
 
 
