@@ -444,7 +444,11 @@ struct DiagSmem {
 // < J and the diagonal block stored by wave 2 in iteration J+1, never the current leaf's rows);
 // bit 1 -- branch-free LDS loads / stores around the leaf (clamped addresses + selects).
 #ifndef IPM_DIAG_V
-#define IPM_DIAG_V 130   // branch-free leaf LDS traffic + look-ahead tiles off wave 3 (tools/chol_lab.hip: 73.0K -> 66.7K cycles)
+// 130: branch-free leaf LDS traffic + look-ahead tiles off wave 3 (tools/chol_lab.hip: 73.0K -> 66.7K
+// cycles); + 65536 lean leaf tail, 262144 L11 written back after the last progress word, 524288
+// later leaves' tiles published by the free waves, 1048576 wave 3 takes a look-ahead tile while two
+// waves run the leaf (r5 stamps, profiles/r5i: time to the role's last progress word 70.1K -> 61.8K)
+#define IPM_DIAG_V (130 + 65536 + 262144 + 524288 + 1048576)
 #endif
 template <bool FUSED = false, int V = 0>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
@@ -733,12 +737,17 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       }
       int bad = 0;
       double dvs[16];
+      // V & 65536 (lean tail): the failure test is one sum of the 16 pivot factors dv (NaN for a
+      // pivot <= 0 or NaN, so the sum is not < inf), read once after the sweep; the exact first
+      // failing column is recovered only on that (rare) path
+      double dsum = 0.0;
       auto sweep = [&]() {
       double piv = readlane_d(row[0], 0);
       double dv = rsqrt_pivot(piv);
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        if (V & 65536) dsum += dv;
+        else if (!(piv > 0.0) && bad == 0) bad = c + 1;
         dvs[c] = dv;
         double pivn = 1.0, dvn = 1.0;
         if (c + 1 < 16) {
@@ -796,16 +805,44 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
         for (int c = 0; c < 16; ++c) { row[c] = row0[c]; rowb[c] = rowb0[c]; }
         bad = 0;
+        dsum = 0.0;
       }
+#ifdef IPM_STAMPS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (stamped lab builds: the sweep alone)
+      STAMPAT(48 + J);
+#endif
       sweep();
+#ifdef IPM_STAMPS
+      STAMPAT(56 + J);
+#endif
       if (bval) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           sD[bb + c * 16 + rr] = rowb[c];
-          if (pubL && !(V & 4096)) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);   // (4096: lab timing only)
+          // (4096: lab timing only; 524288: leaves J >= 2 are published from LDS by the free waves
+          // in the next iteration)
+          if (pubL && !(V & 4096) && !((V & 524288) && J >= 2)) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);
         }
       }
-      if (wv == 0) {
+      if ((V & 65536) && wv == 0) {
+        // the diagonal rows as they are (the upper part of a diagonal block is never read: the
+        // inverse, the write-back and the row roles use its lower part only) and the 16 pivot
+        // factors -- wave-uniform values -- from ONE lane: no per-lane selects
+        if (lane < 16) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = row[c];   // column-major
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) srinv[J * 16 + c] = dvs[c];
+        }
+        if (!(dsum < __builtin_inf())) {   // a pivot <= 0 or NaN (LAPACK potrf's test), rare
+#pragma unroll
+          for (int c = 15; c >= 0; --c)
+            if (!(dvs[c] > 0.0)) bad = c + 1;
+          if (lane == 0) fail = J * 16 + bad;
+        }
+      } else if (wv == 0) {
         if (V & 2) {
           double mine = dvs[0];
 #pragma unroll
@@ -839,9 +876,24 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
         for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
       }
+      if ((V & 524288) && pubL && J >= 3) {
+        // the previous leaf's tiles (I, J-1), I >= J, from LDS to pubL, spread over the free waves:
+        // tile (I, J-1) belongs to block row I, released (progress > I) at the end of iteration I
+        // >= J at the earliest -- after this iteration's store wait and barrier.  (Leaves 0 and 1
+        // publish their own: in iterations 1-2 the free waves have no slack.)
+        const int fw0 = (ONE ? nbt > 3 : nbt > 4) ? 2 : 1;
+        for (int I = J + (wv - fw0); I < 8; I += 4 - fw0) {
+          const int tb = bidx(I, J - 1) * 256;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) st_sc1(&pubL[tb + q * 64 + lane], sD[tb + q * 64 + lane]);
+        }
+      }
       // V & 512: wave 2 writes the whole block column back, so that wave 3's store wait (its
       // vmcnt(0) before the barrier) covers only its Dinv stores
-      if (V & 512) {
+      // (V & 262144: no write-back here -- nothing in the launch reads L11 from A; it goes back
+      // after the role's last progress word, off the chain)
+      if (V & 262144) {
+      } else if (V & 512) {
         if (wv == 2) write_back(J - 1, 0, 1);
       } else if (wv >= 2) {
         write_back(J - 1, wv - 2, 2);
@@ -854,10 +906,11 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       if (V & 256) {
         // greedy list schedule of the look-ahead tiles I = J+1..7 over the free waves, by cost
         // estimates in cycles (lab stamps): the inverse ~4000 (wave 3), publish + write-back
-        // ~1000 (wave 2), a tile ~400 + 250 J; every wave computes the same schedule
+        // ~1000 (wave 2; publish alone ~300 with the write-back deferred), a tile ~400 + 250 J;
+        // every wave computes the same schedule
         int It[6] = {0, 0, 0, 0, 0, 0};
         int nt = 0;
-        int load[4] = {1 << 30, f0 <= 1 ? 0 : (1 << 30), 1000, 4000};
+        int load[4] = {1 << 30, f0 <= 1 ? 0 : (1 << 30), (V & 262144) ? 300 : 1000, 4000};
         for (int I = J + 1; I < 8; ++I) {
           int best = 1;
 #pragma unroll
@@ -869,6 +922,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         if (!(V & 8))
           for (int t0 = 0; t0 < nt; t0 += 3)
             tile_update_multi(It + t0, (1u << std::min(3, nt - t0)) - 1u, J + 1, J);
+      } else if ((V & 1048576) && f0 == 2) {
+        // iterations with two leaf waves (J <= 2): wave 3 (the inverse) also takes the last tile
+        if (!(V & 8) && wv >= 2)
+          for (int I = (wv == 3 ? 7 : J + 1); I < (wv == 3 ? 8 : 7); ++I) tile_update_n(I, J + 1, J);
       } else if (!(V & 8) && !((V & 128) && wv == 3)) {
         for (int I = J + 1 + (wv - f0); I < 8; I += nf) tile_update_n(I, J + 1, J);
       }
@@ -906,7 +963,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
       for (int q = 0; q < 4; ++q) st_sc1(&pubL[db + q * 64 + lane], sD[db + q * 64 + lane]);
     }
-    if (wv == 1) write_back(Jl, 0, 1);   // (block columns 0 .. Jl-1 went back during the loop)
+    if (wv == 1 && !(V & 262144)) write_back(Jl, 0, 1);   // (block columns 0 .. Jl-1 went back during the loop)
   }
   if (pubL) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -914,6 +971,11 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     if (tid == 0) __hip_atomic_store(progress, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   STAMP();
+  if (V & 262144) {
+    // L11 back to A after the last progress word: its readers are the backward solve and later
+    // launches (the row roles and the fold tiles read pubL / the row chunks' outputs)
+    for (int Jc = 0; Jc < nJ; ++Jc) write_back(Jc, wv, 4);
+  }
 }
 #undef STAMP
 

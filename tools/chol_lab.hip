@@ -99,9 +99,12 @@ int main(int argc, char** argv) {
            name, cy[cy.size() / 2], cy[0], us[us.size() / 2], inf, dref / nrm, d0);
   };
   run(k_lab_diag<130>, "V130 shipped (IPM_DIAG_V)");
-  run(k_lab_diag<130 + 32768>, "V130 + ONE register stream (readlane multipliers)");
-  run(k_lab_diag<130 + 16>, "V130 + builtin DPP broadcast shared by both streams");
-  run(k_lab_diag<130 + 64>, "V130 + tile rows through readlane multipliers");
+  run(k_lab_diag<130 + 65536>, "V130 + lean leaf tail");
+  run(k_lab_diag<130 + 65536 + 262144>, "V130 + lean tail + deferred write-back");
+  run(k_lab_diag<130 + 65536 + 262144 + 524288>, "V130 + lean tail + deferred wb + deferred publish J>=2");
+  run(k_lab_diag<130 + 65536 + 262144 + 1048576>, "V130 + lean tail + deferred wb + wave 3 tile at J<=2");
+  run(k_lab_diag<130 + 65536 + 262144 + 524288 + 1048576>, "V130 + lean + dwb + dpub J>=2 + w3 tile");
+  run(k_lab_diag<130 + 65536 + 8>, "V130 + lean tail + free waves idle (timing only)");
   run(k_lab_diag<130>, "V130 shipped (again)");
   return 0;
 }

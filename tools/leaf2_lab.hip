@@ -281,7 +281,11 @@ int main() {
       for (int J = 0; J < 8; ++J)
         printf("  J=%d first (cold) sweep %lld, second (warm) sweep + stores %lld\n", J, (long long)(s[16 + J] - s[2 + 3 * J]),
                (long long)(s[32 + J] - s[16 + J]));
-    printf("   J   step1+bar    leaf(w0)   bar-wait  progress   | inv(w3)  free-waves done (w1 w2 w3) from step1 end\n");
+    printf("   leaf phases per J: step-1 barrier -> LDS operands landed / sweep alone / stores done:");
+    for (int J = 0; J < 8; ++J)
+      printf("  %lld/%lld/%lld", (long long)(s[48 + J] - s[2 + 3 * J]), (long long)(s[56 + J] - s[48 + J]),
+             (long long)(s[32 + J] - s[56 + J]));
+    printf("\n   J   step1+bar    leaf(w0)   bar-wait  progress   | inv(w3)  free-waves done (w1 w2 w3) from step1 end\n");
     for (int J = 0; J < 8; ++J) {
       const unsigned long long st = J == 0 ? s[1] : s[4 + 3 * (J - 1)];
       printf("  %2d  %9lld  %9lld  %9lld  %8lld   | %7lld  %7lld %7lld %7lld\n", J, (long long)(s[2 + 3 * J] - st),
@@ -292,8 +296,8 @@ int main() {
     }
   }
   };
-  stamped(k_stamped<130>, 130);
-  stamped(k_stamped<130 + 8192>, 130 + 8192);
+  stamped(k_stamped<130 + 65536 + 262144 + 1048576>, 130 + 65536 + 262144 + 1048576);
+  stamped(k_stamped<130 + 65536 + 262144 + 524288 + 1048576>, 130 + 65536 + 262144 + 524288 + 1048576);
 
 
 
