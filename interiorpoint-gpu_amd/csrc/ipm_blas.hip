@@ -382,10 +382,14 @@ __device__ __forceinline__ double bcast16(double x, int l) {
   return 0.0;
 }
 
+#if defined(IPM_ROLE_TRACE) && !defined(IPM_STAMPS)
+#define IPM_STAMPS 1   // (the role-trace build also stamps the traced launch's P(a) diagonal role)
+#endif
 #ifdef IPM_STAMPS
+// phase stamps of a diagonal role (labs; the role-trace build: the traced launch's P(a) role)
 __device__ unsigned long long ipm_stamps[128];
-#define STAMP() do { if (tid == 0) ipm_stamps[nst] = __builtin_amdgcn_s_memtime(); ++nst; } while (0)
-#define STAMPAT(i) do { if (lane == 0) ipm_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP() do { if (stamp_on && tid == 0) ipm_stamps[nst] = __builtin_amdgcn_s_memtime(); ++nst; } while (0)
+#define STAMPAT(i) do { if (stamp_on && lane == 0) ipm_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP() do {} while (0)
 #define STAMPAT(i) do {} while (0)
@@ -414,10 +418,10 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
 #pragma unroll
     for (int k = 0; k < r; ++k) v = fma(-sblk[k * 16 + r], x[k], v);
     x[r] = (r >= c) ? v * rinv[r] : 0.0;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    // each row stored as soon as it is final: inside the fused factorization these sc1 stores
+    // go to a loaded memory system, and the role's end-of-iteration store wait then covers only
+    // the last rows instead of all 16 (r5k: the wait was 1.3-2.2K cycles per iteration)
+    if (lane < 16) {
       if (sc1) st_sc1(&out[c * 16 + r], x[r]);
       else out[c * 16 + r] = x[r];
     }
@@ -454,7 +458,8 @@ template <bool FUSED = false, int V = 0>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
                                           double* __restrict__ dinv_out, int* __restrict__ info,
                                           double* pubL, unsigned* progress, DiagSmem& sm,
-                                          unsigned* failw = nullptr) {
+                                          unsigned* failw = nullptr, bool stamp_on = true) {
+  (void)stamp_on;
   double* sD = sm.sD;
   double* srinv = sm.srinv;
   int& fail = sm.fail;
@@ -1425,7 +1430,12 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     else wait_la(0, b.wa - 1);
     // (the round-4 one-sweep role, tools/diag2_lab.hip + ipm_diag2.h, ran 5 % faster alone but not
     // inside the launch, and instantiating it here raised the kernel's SGPR spills 80 -> 700+)
-    diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL]);
+#ifdef IPM_ROLE_TRACE
+    diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL],
+                                b.trace != 0 && !pb);
+#else
+    diag_role<true, IPM_DIAG_V>(kp, nbp, b.A, b.lda, ws, b.info, ws + PF_DINV, prog, sm.d, &b.ctl[CTL_FAIL], false);
+#endif
     return;
   }
   if (kind == K_ROW) {
@@ -2238,6 +2248,9 @@ static int num_cus() {
   return ncu;
 }
 #ifdef IPM_ROLE_TRACE
+extern "C" int ipm_debug_diag_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_stamps), sizeof(unsigned long long) * 128);
+}
 extern "C" int ipm_debug_role_trace(unsigned long long* out, int n_wg) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_role_trace), sizeof(unsigned long long) * 4 *
                                                                        std::min(n_wg, 8192));

@@ -105,9 +105,12 @@ class Shard:
         self.dev = local_device(device)
         self.concurrent = bool(concurrent)
         # batched Cholesky (ipm_potrf_batch): the concurrent instances' factorizations run as one
-        # launch per 256-column block (default with concurrent=True; IPM_POTRF_BATCH=0 turns it off)
+        # launch per 256-column block.  Opt-in (batch=True or IPM_POTRF_BATCH=1): measured on config 4
+        # (8 x n=2048, r5d) it LOSES -- 1647-1774 Newton it/s against 3107-3122 without it: the
+        # rendezvous puts every instance in lockstep, so the latency-bound small kernels of all
+        # instances run in the same phase instead of filling the gaps of the others' Cholesky chains.
         if batch is None:
-            batch = self.concurrent and os.environ.get("IPM_POTRF_BATCH", "1") != "0"
+            batch = self.concurrent and os.environ.get("IPM_POTRF_BATCH", "0") == "1"
         self.batch = None
         self.streams = ([torch.cuda.Stream(device=torch.device("cuda", self.dev)) for _ in self.indices]
                         if self.concurrent else [None] * len(self.indices))

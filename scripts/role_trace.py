@@ -46,3 +46,21 @@ for row in s[np.argsort(s[:, 3])]:
     wake, loaded = row[3], row[1] + (row[0] & 0xFFFFFFFF)
     if 0 < wake - t0 < 10 ** 9:
         print(f"    NF tile wake {(wake - t0) / 100:6.1f}  loaded {(loaded - t0) / 100:6.1f}  end {(row[2] - t0) / 100:6.1f}")
+
+# the traced launch's P(a) diagonal role, stamped inside the fused kernel (s_memtime cycles; the
+# same phases as tools/leaf2_lab.hip prints for the role alone)
+st = (ctypes.c_ulonglong * 128)()
+if hasattr(h.lib, "ipm_debug_diag_stamps") and h.lib.ipm_debug_diag_stamps(st) == 0:
+    s = np.frombuffer(st, dtype=np.uint64).astype(np.int64)
+    if s[0] > 0 and s[26] > s[0]:
+        print(f"  P(a) diagonal role in the launch: {s[26] - s[0]} cycles to its last progress word, "
+              f"panel load {s[1] - s[0]}")
+        print("   leaf phases per J: operands landed / sweep / stores:",
+              "  ".join(f"{s[48 + J] - s[2 + 3 * J]}/{s[56 + J] - s[48 + J]}/{s[32 + J] - s[56 + J]}" for J in range(8)))
+        print("   J  step1+bar  leaf(w0)  bar-wait  progress | inv(w3)  free waves done (w1 w2 w3), from step-1 end")
+        for J in range(8):
+            st0 = s[1] if J == 0 else s[4 + 3 * (J - 1)]
+            b = s[2 + 3 * J]
+            fw = " ".join(f"{s[80 + 8 * w + J] - b:7d}" for w in (1, 2, 3)) if J else ""
+            print(f"  {J:2d} {b - st0:9d} {s[32 + J] - b:9d} {s[3 + 3 * J] - s[32 + J]:9d} "
+                  f"{s[4 + 3 * J] - s[3 + 3 * J]:9d} | {(s[40 + J] - b) if J else 0:7d}  {fw}")
