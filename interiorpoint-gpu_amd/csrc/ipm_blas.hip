@@ -428,6 +428,18 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
   }
 }
 
+// Dinv_J computed by the leaf (row-major in LDS, element (r, c) at 16 r + c) -> out, column-major
+// (element (r, c) at 16 c + r), one wave
+__device__ __forceinline__ void publish_dinv(const double* t, double* out, int lane, bool sc1) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int gi = q * 64 + lane;
+    const double v = t[(gi & 15) * 16 + (gi >> 4)];
+    if (sc1) st_sc1(&out[gi], v);
+    else out[gi] = v;
+  }
+}
+
 // One workgroup, 4 waves.  Chain per 16-column block J: MFMA update of block column J ->
 // wave 0 factors L_JJ in registers -> waves 0-1 solve the tiles below by substitution.  The
 // inverses Dinv_J the TRSM kernel needs are computed by wave 3 while wave 0 factors the NEXT
@@ -438,6 +450,7 @@ __device__ __forceinline__ void tri_inverse16(const double* sblk, const double* 
 struct DiagSmem {
   double sD[36 * 256];   // L11 (identity-padded beyond nb)
   double srinv[8 * 16];  // 1 / L_cc per diagonal block
+  double sdinv[2 * 256];  // V & 2097152: Dinv_J from the leaf (row-major), double-buffered by J
   int fail;
 };
 
@@ -447,12 +460,17 @@ struct DiagSmem {
 // published stores at the end of an iteration (progress J+1 needs block row J: tiles from leaves
 // < J and the diagonal block stored by wave 2 in iteration J+1, never the current leaf's rows);
 // bit 1 -- branch-free LDS loads / stores around the leaf (clamped addresses + selects).
+#ifndef IPM_FOLD_ACC
+#define IPM_FOLD_ACC 1
+#endif
 #ifndef IPM_DIAG_V
 // 130: branch-free leaf LDS traffic + look-ahead tiles off wave 3 (tools/chol_lab.hip: 73.0K -> 66.7K
 // cycles); + 65536 lean leaf tail, 262144 L11 written back after the last progress word, 524288
 // later leaves' tiles published by the free waves, 1048576 wave 3 takes a look-ahead tile while two
-// waves run the leaf (r5 stamps, profiles/r5i: time to the role's last progress word 70.1K -> 61.8K)
-#define IPM_DIAG_V (130 + 65536 + 262144 + 524288 + 1048576)
+// waves run the leaf (r5 stamps, profiles/r5i: time to the role's last progress word 70.1K -> 61.8K);
+// + 2097152 Dinv from the leaf sweep (profiles/r5m: in the launch 69.8K -> 57.1K stamped cycles,
+// POTRF n = 2048 0.713 -> 0.638 ms, the factor bitwise unchanged)
+#define IPM_DIAG_V (130 + 65536 + 262144 + 524288 + 1048576 + 2097152)
 #endif
 template <bool FUSED = false, int V = 0>
 __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict__ A, int64_t lda,
@@ -675,8 +693,14 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     // same arithmetic as the two-stream sweep (same fma operands).  Leaf waves: 0, 1 while more
     // than 3 tiles are below, 2 for the seventh (J = 0, when waves 2-3 have no other work).
     constexpr bool ONE = (V & 32768) != 0;
+    // V & 2097152 (Dinv from the leaf): the lane group after the last tile (Ib == 8) sweeps the
+    // identity rows, X = I L^-T: lane r ends with column r of Dinv = L^-1, by the same fma
+    // sequence as tri_inverse16 (operand by operand: starts at d_rc, subtracts L[r][k] x[k] for
+    // k = 0, 1, .. in order, scales by the pivot factor) -- bitwise the same inverse, and wave 3 is
+    // free.  Needs a second leaf wave at J = 3 (wave 0's four groups hold tiles 4-7).
+    constexpr bool DL = (V & 2097152) != 0;
     const bool leafw = ONE ? (wv == 0 || (wv == 1 && nbt > 3) || (wv == 2 && nbt > 6))
-                           : ((wv == 0) || (wv == 1 && nbt > 4));
+                           : ((wv == 0) || (wv == 1 && (nbt > 4 || (DL && nbt == 4))));
     if (ONE && leafw) {
       const int db = bidx(J, J) * 256;
       const int rr = lane & 15, g = lane >> 4;
@@ -732,6 +756,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       const int rr = lane & 15;
       const int Ib = J + 1 + 4 * wv + (lane >> 4);
       const bool bval = Ib < 8;
+      const bool idg = DL && Ib == 8;
       const int bb = bidx(bval ? Ib : J, J) * 256;
       double row[16], rowb[16];
 #pragma unroll
@@ -739,6 +764,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         row[c] = sD[db + c * 16 + rr];
         if (V & 2) rowb[c] = sD[bb + c * 16 + rr];   // bb == db for absent tiles: a harmless copy
         else rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
+        if (DL) rowb[c] = idg ? (c == rr ? 1.0 : 0.0) : rowb[c];
       }
       int bad = 0;
       double dvs[16];
@@ -820,7 +846,17 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #ifdef IPM_STAMPS
       STAMPAT(56 + J);
 #endif
-      if (bval) {
+      if (DL && (bval || idg)) {
+        // tile rows to their block; the identity group's Dinv rows -- lane r holds Dinv[c][r] --
+        // to sdinv row-major (element (c, r) at 16 c + r): one store stream, no divergence
+        double* dst = bval ? &sD[bb] : &sm.sdinv[(J & 1) * 256];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) dst[c * 16 + rr] = rowb[c];
+        if (bval && pubL && !(V & 4096) && !((V & 524288) && J >= 2)) {
+#pragma unroll
+          for (int c = 0; c < 16; ++c) st_sc1(&pubL[bb + c * 16 + rr], rowb[c]);
+        }
+      } else if (bval) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
           sD[bb + c * 16 + rr] = rowb[c];
@@ -871,7 +907,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       // the other waves, off the chain: wave 3 inverts the PREVIOUS diagonal block for the row
       // part; wave 2 publishes it and writes block column J-1 back to A; the free waves apply
       // terms 0..J-1 to the tiles of block column J+1 (look-ahead)
-      if (wv == 3 && !(V & 8)) {   // (V & 8: lab timing only -- the free waves skip their work)
+      if (DL && wv == 3) {
+        publish_dinv(&sm.sdinv[((J - 1) & 1) * 256], dinv_out + (J - 1) * 256, lane, pubL != nullptr);
+        STAMPAT(40 + J);
+      } else if (wv == 3 && !(V & 8)) {   // (V & 8: lab timing only -- the free waves skip their work)
         tri_inverse16(&sD[bidx(J - 1, J - 1) * 256], &srinv[(J - 1) * 16], dinv_out + (J - 1) * 256, lane,
                       pubL != nullptr);
         STAMPAT(40 + J);
@@ -886,7 +925,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         // tile (I, J-1) belongs to block row I, released (progress > I) at the end of iteration I
         // >= J at the earliest -- after this iteration's store wait and barrier.  (Leaves 0 and 1
         // publish their own: in iterations 1-2 the free waves have no slack.)
-        const int fw0 = (ONE ? nbt > 3 : nbt > 4) ? 2 : 1;
+        const int fw0 = (ONE ? nbt > 3 : (nbt > 4 || (DL && nbt == 4))) ? 2 : 1;
         for (int I = J + (wv - fw0); I < 8; I += 4 - fw0) {
           const int tb = bidx(I, J - 1) * 256;
 #pragma unroll
@@ -906,9 +945,13 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       STAMPAT(64 + 8 * wv + J);
       // free waves: {1, 2, 3} or {2, 3}; tile I = J+1.. round robin.  V & 128: wave 3 (the
       // inverse, ~3900 cycles) takes no look-ahead tiles -- they go to the other free waves
-      const int f0 = (ONE ? nbt > 3 : nbt > 4) ? 2 : 1;
+      const int f0 = (ONE ? nbt > 3 : (nbt > 4 || (DL && nbt == 4))) ? 2 : 1;
       const int nf = (V & 128) ? 3 - f0 : 4 - f0;
-      if (V & 256) {
+      if (DL) {
+        // wave 3 publishes Dinv only (4 stores): all free waves share the tiles round robin
+        if (!(V & 8))
+          for (int I = J + 1 + (wv - f0); I < 8; I += 4 - f0) tile_update_n(I, J + 1, J);
+      } else if (V & 256) {
         // greedy list schedule of the look-ahead tiles I = J+1..7 over the free waves, by cost
         // estimates in cycles (lab stamps): the inverse ~4000 (wave 3), publish + write-back
         // ~1000 (wave 2; publish alone ~300 with the write-back deferred), a tile ~400 + 250 J;
@@ -962,7 +1005,10 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   }
   {
     const int Jl = nJ - 1;   // the last block column (7 for a full panel)
-    if (wv == 3) tri_inverse16(&sD[bidx(Jl, Jl) * 256], &srinv[Jl * 16], dinv_out + Jl * 256, lane, pubL != nullptr);
+    if (wv == 3) {
+      if (V & 2097152) publish_dinv(&sm.sdinv[(Jl & 1) * 256], dinv_out + Jl * 256, lane, pubL != nullptr);
+      else tri_inverse16(&sD[bidx(Jl, Jl) * 256], &srinv[Jl * 16], dinv_out + Jl * 256, lane, pubL != nullptr);
+    }
     if (wv == 2 && pubL) {
       const int db = bidx(Jl, Jl) * 256;
 #pragma unroll
@@ -1255,7 +1301,12 @@ struct RoleTrace {
 };
 #define ROLE(r) (rt.role = (r))
 #define ROLE_STAMP(f) (rt.f = __builtin_amdgcn_s_memrealtime())
+// look-ahead fold tiles of the traced launch: [tile][0] start, 1 wake, 2 + 2p operands of pass p
+// in LDS, 3 + 2p its MFMAs issued, 10 stores done, 11 fnp  (s_memrealtime ticks)
+__device__ unsigned long long ipm_fold_trace[16 * 12];
+#define FOLD_STAMP(i) do { if (rt.on && frole == 0 && ftile < 16 && tid == 0) ipm_fold_trace[ftile * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define FOLD_STAMP(i) do {} while (0)
 #define ROLE(r) ((void)0)
 #define ROLE_STAMP(f) ((void)0)
 #endif
@@ -1274,15 +1325,17 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
 #ifdef IPM_ROLE_TRACE
   RoleTrace rt(b.trace != 0, (int)t);
 #endif
-  {
-    // a failure in an earlier launch: pass it on and stop (consistent for every workgroup:
-    // the word was final before this launch started)
-    const unsigned pf = ld_ctl(const_cast<unsigned*>(b.prevfail));
-    if (pf != 0) {
-      if (t == 0 && tid == 0) __hip_atomic_store(&b.ctl[CTL_FAIL], pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
+  // a failure in an earlier launch: pass it on and stop (consistent for every workgroup: the
+  // word was final before this launch started).  The look-ahead fold tiles test it after their
+  // first operand loads are in flight (the word's latency hidden behind theirs).
+  const int64_t t_launch = t;
+  const unsigned pf = ld_ctl(const_cast<unsigned*>(b.prevfail));
+  auto prev_failed = [&]() {
+    if (pf == 0) return false;
+    if (t_launch == 0 && tid == 0) __hip_atomic_store(&b.ctl[CTL_FAIL], pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
+  if (!(VEC && t < b.nla32 && (b.la32.K % 128) == 0) && prev_failed()) return;
   unsigned* la_done = b.ctl + CTL_HDR;
   unsigned* pa_done = la_done + (b.n + 63) / 64;
   // look-ahead tiles: the first 128 rows x 128 columns (what the P(a) diagonal role waits for,
@@ -1471,6 +1524,13 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
       __syncthreads();
     }
     ROLE_STAMP(wake);
+#ifdef IPM_ROLE_TRACE
+    if (rt.on && frole == 0 && ftile < 16 && tid == 0) {
+      ipm_fold_trace[ftile * 12] = rt.t0;
+      ipm_fold_trace[ftile * 12 + 11] = (unsigned long long)fnp;
+    }
+#endif
+    FOLD_STAMP(1);
     const int lane = tid & 63, wv = tid >> 6, fr = lane & 15, fk = lane >> 4;
     const int ib = 32 * ti + 16 * (wv & 1), jb = 32 * tj + 16 * (wv >> 1);
     const bool live = ib + 15 >= jb;   // sub-tiles entirely above the diagonal are never read
@@ -1493,8 +1553,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
       // masked.
       double* sL = sm.d.sD;
       const int nsrc = ti == tj ? 1 : 2;
-      for (int p = 0; p < fnp; ++p) {
-        if (p) __syncthreads();   // (the previous pass's operands are consumed)
+      auto issue = [&](int p) {
         for (int it = wv; it < 32 * nsrc; it += 4) {
           const int sblk = it >> 5, c4 = it & 31;
           const int col = 128 * p + 4 * c4 + (lane >> 4);
@@ -1503,20 +1562,60 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
                                            (__attribute__((address_space(3))) void*)&sL[sblk * 4096 + c4 * 128], 16,
                                            0, 16);   // aux 16 = sc1
         }
+      };
+      const double* sa = sL + 16 * (wv >> 1) + fr;                          // L[jb + fr][k] at sa[32 k]
+      const double* sbp = sL + (ti == tj ? 0 : 4096) + 16 * (wv & 1) + fr;   // L[i][k]
+      // IPM_FOLD_ACC > 1: the MFMA chain over that many accumulators (k interleaved; not bitwise
+      // the single-chain sum)
+      dbl4 xacc[3] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};
+      issue(0);
+      if (la_fold && prev_failed()) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (no LDS writes in flight at exit)
+        return;
+      }
+      // per pass: operands LDS -> registers, then (all waves past a barrier) the next pass's loads
+      // go out while this pass's MFMA chain runs from registers.  (r5n trace: with the LDS reads
+      // inside the chain a pass's 32 MFMAs took ~3 us, and loads and MFMAs alternated.)
+      for (int p = 0; p < fnp; ++p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         ROLE_STAMP(loaded);
+        if (p < 4) FOLD_STAMP(2 + 2 * p);
+        // unconditional LDS reads (in bounds; masked rows hold matrix data) and selects after them:
+        // a masked read is a branch, and each one waited for its value (64 serialized LDS
+        // latencies per pass, ~2 us)
+        double av[32], bv[32];
         if (live) {
-          const double* sa = sL + 16 * (wv >> 1) + fr;                          // L[jb + fr][k] at sa[32 k]
-          const double* sbp = sL + (ti == tj ? 0 : 4096) + 16 * (wv & 1) + fr;   // L[i][k]
 #pragma unroll
           for (int qq = 0; qq < 32; ++qq) {
             const int k = 4 * qq + fk;
-            const double av = jin ? -sa[32 * k] : 0.0, bv = iin ? sbp[32 * k] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            av[qq] = sa[32 * k];
+            bv[qq] = sbp[32 * k];
+          }
+#pragma unroll
+          for (int qq = 0; qq < 32; ++qq) {
+            av[qq] = jin ? -av[qq] : 0.0;
+            bv[qq] = iin ? bv[qq] : 0.0;
           }
         }
+        if (p + 1 < fnp) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __syncthreads();   // every wave holds this pass's operands: the buffer is free
+          issue(p + 1);
+        }
+        if (live) {
+#pragma unroll
+          for (int qq = 0; qq < 32; ++qq) {
+            dbl4& a = (IPM_FOLD_ACC == 1 || qq % IPM_FOLD_ACC == 0) ? acc : xacc[qq % IPM_FOLD_ACC - 1];
+            a = __builtin_amdgcn_mfma_f64_16x16x4f64(av[qq], bv[qq], a, 0, 0, 0);
+          }
+        }
+#ifdef IPM_ROLE_TRACE
+        if (p < 4) { asm volatile("s_nop 0" ::"v"(acc[0])); FOLD_STAMP(3 + 2 * p); }
+#endif
       }
+      if (IPM_FOLD_ACC == 2) acc = acc + xacc[0];
+      if (IPM_FOLD_ACC == 4) acc = (acc + xacc[0]) + (xacc[1] + xacc[2]);
     } else if (live) {
       // (NF only: unaligned operands never take the look-ahead path above)
       const double* pa = b.A + fsrc * b.lda + fo + jb + fr;   // L[jb + fr][k] at pa[k * lda]
@@ -1541,6 +1640,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    FOLD_STAMP(10);
     if (tid == 0) __hip_atomic_fetch_add(fdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
@@ -2250,6 +2350,15 @@ static int num_cus() {
 #ifdef IPM_ROLE_TRACE
 extern "C" int ipm_debug_diag_stamps(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_stamps), sizeof(unsigned long long) * 128);
+}
+extern "C" int ipm_debug_fold_trace(unsigned long long* out) {
+#ifdef IPM_ROLE_TRACE
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_fold_trace), sizeof(unsigned long long) * 16 * 12, 0,
+                                  hipMemcpyDeviceToHost);
+#else
+  (void)out;
+  return -1;
+#endif
 }
 extern "C" int ipm_debug_role_trace(unsigned long long* out, int n_wg) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_role_trace), sizeof(unsigned long long) * 4 *
