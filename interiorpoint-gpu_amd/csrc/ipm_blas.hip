@@ -1301,10 +1301,11 @@ struct RoleTrace {
 };
 #define ROLE(r) (rt.role = (r))
 #define ROLE_STAMP(f) (rt.f = __builtin_amdgcn_s_memrealtime())
-// look-ahead fold tiles of the traced launch: [tile][0] start, 1 wake, 2 + 2p operands of pass p
-// in LDS, 3 + 2p its MFMAs issued, 10 stores done, 11 fnp  (s_memrealtime ticks)
-__device__ unsigned long long ipm_fold_trace[16 * 12];
-#define FOLD_STAMP(i) do { if (rt.on && frole == 0 && ftile < 16 && tid == 0) ipm_fold_trace[ftile * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// fold tiles of the traced launch (slots 0-15 look-ahead, 16-31 NF): [slot][0] start, 1 wake,
+// 2 + 2p operands of pass p in LDS, 3 + 2p its MFMAs done, 10 stores done, 11 fnp  (s_memrealtime)
+__device__ unsigned long long ipm_fold_trace[32 * 12];
+#define FOLD_SLOT ((frole == 0 ? 0 : 16) + ftile)
+#define FOLD_STAMP(i) do { if (rt.on && ftile < 16 && tid == 0) ipm_fold_trace[FOLD_SLOT * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define FOLD_STAMP(i) do {} while (0)
 #define ROLE(r) ((void)0)
@@ -1328,9 +1329,11 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   // a failure in an earlier launch: pass it on and stop (consistent for every workgroup: the
   // word was final before this launch started).  The look-ahead fold tiles test it after their
   // first operand loads are in flight (the word's latency hidden behind theirs).
+  // (r5q trace: the test's load, waited for at once to branch on, held every workgroup ~1.2 us at
+  // the launch start)
   const int64_t t_launch = t;
-  const unsigned pf = ld_ctl(const_cast<unsigned*>(b.prevfail));
   auto prev_failed = [&]() {
+    const unsigned pf = ld_ctl(const_cast<unsigned*>(b.prevfail));
     if (pf == 0) return false;
     if (t_launch == 0 && tid == 0) __hip_atomic_store(&b.ctl[CTL_FAIL], pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
@@ -1525,9 +1528,9 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     }
     ROLE_STAMP(wake);
 #ifdef IPM_ROLE_TRACE
-    if (rt.on && frole == 0 && ftile < 16 && tid == 0) {
-      ipm_fold_trace[ftile * 12] = rt.t0;
-      ipm_fold_trace[ftile * 12 + 11] = (unsigned long long)fnp;
+    if (rt.on && ftile < 16 && tid == 0) {
+      ipm_fold_trace[FOLD_SLOT * 12] = rt.t0;
+      ipm_fold_trace[FOLD_SLOT * 12 + 11] = (unsigned long long)fnp;
     }
 #endif
     FOLD_STAMP(1);
@@ -2353,7 +2356,7 @@ extern "C" int ipm_debug_diag_stamps(unsigned long long* out) {
 }
 extern "C" int ipm_debug_fold_trace(unsigned long long* out) {
 #ifdef IPM_ROLE_TRACE
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_fold_trace), sizeof(unsigned long long) * 16 * 12, 0,
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_fold_trace), sizeof(unsigned long long) * 32 * 12, 0,
                                   hipMemcpyDeviceToHost);
 #else
   (void)out;

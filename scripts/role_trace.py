@@ -66,14 +66,14 @@ if hasattr(h.lib, "ipm_debug_diag_stamps") and h.lib.ipm_debug_diag_stamps(st) =
                   f"{s[4 + 3 * J] - s[3 + 3 * J]:9d} | {(s[40 + J] - b) if J else 0:7d}  {fw}")
 
 # look-ahead fold tiles (the P(a) diagonal block's 32-tiles): per tile, us from the launch start
-ft = (ctypes.c_ulonglong * (16 * 12))()
+ft = (ctypes.c_ulonglong * (32 * 12))()
 if hasattr(h.lib, "ipm_debug_fold_trace") and h.lib.ipm_debug_fold_trace(ft) == 0:
-    f = np.frombuffer(ft, dtype=np.uint64).reshape(16, 12).astype(np.int64)
-    for i in range(16):
+    f = np.frombuffer(ft, dtype=np.uint64).reshape(32, 12).astype(np.int64)
+    for i in range(32):
         r = f[i]
         if r[0] <= 0 or not (0 <= r[0] - t0 < 10 ** 8):
             continue
         npass = int(r[11])
         us = lambda v: f"{(v - t0) / 100:6.1f}" if v > 0 else "   -  "
         ps = "  ".join(f"p{p} ld {us(r[2 + 2 * p])} mf {us(r[3 + 2 * p])}" for p in range(min(npass, 4)))
-        print(f"    fold tile {i:2d} K={128 * npass:4d} start {us(r[0])} wake {us(r[1])}  {ps}  done {us(r[10])}")
+        print(f"    {'fold' if i < 16 else 'NF  '} tile {i % 16:2d} K={128 * npass:4d} start {us(r[0])} wake {us(r[1])}  {ps}  done {us(r[10])}")
