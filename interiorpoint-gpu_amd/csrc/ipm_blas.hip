@@ -1039,7 +1039,8 @@ enum {
   // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
   // by a workgroup that landed on that CU
   CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
-  CTL_HDR = CTL_SPILL + NCRIT
+  CTL_PB0 = CTL_SPILL + NCRIT,        // P(b)'s first row chunk done (the tail role waits for it)
+  CTL_HDR = CTL_PB0 + 1
 };
 
 // Row role: rows below the diagonal block, L21 = A21 L11^-T, 64 rows per workgroup, 16 rows per
@@ -1250,6 +1251,12 @@ struct BlockArgs {
   GemmArgs s2;
   int rag_K = CH_NB;            // ragged rows: K extent and first column of the applied blocks
   int64_t rag_cp = 0;
+  // tail (potrf_plan): the factorization's last tail_r <= 8 columns (tail_R <= 16 rows from tail_o
+  // on, the bordered right-hand-side row included) are finished by ONE workgroup of the launch
+  // before them instead of a launch of their own: it applies L's columns [tail_k0, tail_k0 +
+  // tail_K) to the corner and factors it
+  int ntail = 0, tail_r = 0, tail_R = 0, tail_K = 0;
+  int64_t tail_o = 0, tail_k0 = 0;
 };
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
 __device__ __forceinline__ unsigned cu_key() {
@@ -1421,7 +1428,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   // could use.  Decode first, then ONE call site per role (each role's code is inlined once:
   // register pressure and code size).
   const int nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_RAG, K_NONE } kind = K_NONE;
+  enum { K_DIAG, K_ROW, K_NF, K_TILE, K_RAG, K_TAIL, K_NONE } kind = K_NONE;
   bool pb = false;       // the role belongs to P(b)
   int64_t chunk = 0;
   if (la_fold) {
@@ -1459,6 +1466,8 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
         kind = K_ROW;
         pb = true;
         chunk = t;
+      } else if ((t -= b.nrb) < b.ntail) {
+        kind = K_TAIL;
       }
     }
   }
@@ -1506,7 +1515,8 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
       wait_la(r0, std::min<int64_t>(r0 + PF_RB, b.n - b.cb) - 1);
     }
     row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
-                   sm.d.sD, &sflag, pb ? nullptr : &pa_done[chunk], false, b.info, failw);
+                   sm.d.sD, &sflag, pb ? (chunk == 0 && b.ntail ? &b.ctl[CTL_PB0] : nullptr) : &pa_done[chunk], false,
+                   b.info, failw);
     return;
   }
   if (kind == K_NF) {
@@ -1647,6 +1657,55 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     if (tid == 0) __hip_atomic_fetch_add(fdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  if (kind == K_TAIL) {
+    ROLE(13);
+    // the corner rows [o, o + R) x columns [o, o + r): C -= L L^T over columns [k0, k0 + K) (the
+    // previous block's, final since the previous launch, and this launch's, final once P(b)'s
+    // first row chunk -- the last rows' -- is done), then a left-looking Cholesky of its r columns
+    // with the diagonal role's pivot factor (L_jj = piv dv, L_ij = v dv, dv = rsqrt_pivot(piv))
+    wait_words(&b.ctl[CTL_PB0], 1, 1u, b.info, failw);
+    const int R = b.tail_R, r = b.tail_r, K = b.tail_K;
+    const int64_t o = b.tail_o, k0 = b.tail_k0, lda = b.lda;
+    double* Ls = sm.d.sD;        // Ls[i K + k] = L(o + i, k0 + k)
+    double* Cs = Ls + R * K;     // Cs[i r + j]: the updated corner, then L
+    double* Ts = Cs + R * r;     // one column's values
+    for (int e = tid; e < R * K; e += 256) {
+      const int k = e / R, i = e - k * R;
+      Ls[i * K + k] = ld_sc1(&b.A[(k0 + k) * lda + o + i]);
+    }
+    __syncthreads();
+    for (int p0 = 0; p0 < R * r; p0 += 16) {   // 16 lanes per (i, j), fixed-order reduction
+      const int p = p0 + (tid >> 4), q = tid & 15, i = p / r, j = p - i * r;
+      const bool live = p < R * r && j <= i;
+      double acc = 0.0;
+      if (live)
+        for (int k = q; k < K; k += 16) acc = fma(Ls[i * K + k], Ls[j * K + k], acc);
+#pragma unroll
+      for (int m = 8; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 16);
+      if (live && q == 0) Cs[i * r + j] = ld_sc1(&b.A[(o + j) * lda + o + i]) - acc;
+    }
+    __syncthreads();
+    int fcol = 0;
+    for (int j = 0; j < r; ++j) {
+      if (tid >= j && tid < R) {
+        double v = Cs[tid * r + j];
+        for (int k = 0; k < j; ++k) v = fma(-Cs[tid * r + k], Cs[j * r + k], v);
+        Ts[tid] = v;
+      }
+      __syncthreads();
+      const double piv = Ts[j], dv = rsqrt_pivot(piv);
+      if (!(piv > 0.0) && fcol == 0) fcol = j + 1;
+      if (tid >= j && tid < R) Cs[tid * r + j] = tid == j ? piv * dv : Ts[tid] * dv;
+      __syncthreads();
+    }
+    if (tid < R)
+      for (int j = 0; j < r && j <= tid; ++j) b.A[(o + j) * lda + o + tid] = Cs[tid * r + j];
+    if (fcol && tid == 0) {
+      atomicCAS(b.info, 0, (int)(o + fcol));
+      __hip_atomic_store(failw, (unsigned)(o + fcol), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (kind == K_RAG) {
     ROLE(12);
     // ragged rows i in [r0, r0 + rn) of the trailing update (origin o, K = the previous block's
@@ -1764,7 +1823,7 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
 // residency), and every instance runs its own plan: results are bitwise those of its own launch.
 // dec: [0, K) global start of (class c, instance i) at c * B + i (non-decreasing), [K, 2K) the
 // launch-local ticket of that class's first item; K = POTRF_NCLS * B.
-constexpr int POTRF_NCLS = 9;
+constexpr int POTRF_NCLS = 10;
 template <bool VEC, bool FASTS = false, int LAZY = 0>
 __global__ __launch_bounds__(256, 2) void k_potrf_batch(const BlockArgs* __restrict__ tab, const int* __restrict__ dec,
                                                         int B, unsigned* gticket) {
@@ -1969,7 +2028,22 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
   const bool lazy_on = !(elz && elz[0] == '0');
   const bool lazy2_on = lazy_on && !(elz && elz[0] == '1');   // IPM_LAZYC=1: K = 256 tiles only
   PairPlan pl = potrf_pair_plan(n, ncols, nblocks);
-  for (int64_t bk = 0; bk < nblocks; ++bk) {
+  // a last block of at most 8 columns with at most 16 rows below its origin (the bordered phase-1
+  // system: 1 column, 2 rows) is finished inside the launch before it by one tail workgroup: its
+  // own launch (look-ahead fold, a diagonal role for one column, the launch boundary) cost ~90 us
+  // per factorization (r5u: phase-1 POTRF 0.764 vs 0.672 ms at n = 2048).  IPM_TAIL=0: off.
+  const char* etl = getenv("IPM_TAIL");
+  const bool tail_on = !(etl && etl[0] == '0');
+  int64_t nemit = nblocks;
+  int tail_r = 0;
+  if (tail_on && nblocks >= 2 && pl.kind[nblocks - 2] == 0) {
+    const int64_t cbl = (nblocks - 1) * CH_NB;
+    if (ncols - cbl <= 8 && n - cbl <= 16) {
+      nemit = nblocks - 1;
+      tail_r = (int)(ncols - cbl);
+    }
+  }
+  for (int64_t bk = 0; bk < nemit; ++bk) {
     const int kind = pl.kind[bk];
     const int64_t Kla = kind == 2 ? 2 * CH_NB : CH_NB;   // look-ahead depth (EVEN: the pair)
     BlockArgs b;
@@ -2138,6 +2212,18 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
         b.s_full = b.ns;
       }
     }
+    if (tail_r > 0 && bk == nemit - 1) {
+      // the trailing region of this launch is exactly the corner: the tail role replaces its
+      // trailing tiles / ragged rows
+      b.ns = b.s_full = b.nstrip = 0;
+      b.nrag = 0;
+      b.ntail = 1;
+      b.tail_r = tail_r;
+      b.tail_o = cb + CH_NB;
+      b.tail_R = (int)(n - b.tail_o);
+      b.tail_k0 = bk > 0 ? cb - CH_NB : 0;
+      b.tail_K = (int)(b.tail_o - b.tail_k0);
+    }
 #ifdef IPM_ROLE_TRACE
     {
       static const int tb = [] { const char* e = getenv("IPM_TRACE_BLOCK"); return e ? atoi(e) : -1; }();
@@ -2185,7 +2271,7 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
       b.sflag = b.ctl + block_ctl_words(n) - potrf_split_cap(n);
     }
     BlockLaunch L;
-    L.grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns;
+    L.grid = b.nla + 1 + b.nra + b.nnf + (b.wbw > 0 ? 1 + b.nrb : 0) + b.nrag + b.ns + b.ntail;
     // all trailing tiles full (rows a multiple of 128 once the ragged rows are split off) -> the
     // branch-free tile loop (IPM_FASTS=0: never)
     const bool fasts = fasts_on && b.ns > 0 && (b.s.ni % 128) == 0 && (b.s.K % 32) == 0;
@@ -2196,7 +2282,7 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
     L.inst = (vec && lazy) ? 0 : (vec && lazy2) ? 1 : (vec && fasts) ? 2 : vec ? 3 : 4;
     // ticket classes in launch-local order (potrf_block_body's decode)
     const int64_t nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-    const int64_t cls[POTRF_NCLS] = {b.nla, 1, nchd, b.nnf, b.wbw > 0 ? 1 : 0, b.nrag, b.ns, b.nra - nchd, b.nrb};
+    const int64_t cls[POTRF_NCLS] = {b.nla, 1, nchd, b.nnf, b.wbw > 0 ? 1 : 0, b.nrag, b.ns, b.nra - nchd, b.nrb, b.ntail};
     for (int c = 0; c < POTRF_NCLS; ++c) L.cls[c] = cls[c];
     L.b = b;
     out.push_back(L);

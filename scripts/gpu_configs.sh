@@ -18,8 +18,10 @@ run() {   # name, bench args
   [ $rc -ne 0 ] && { tail -5 $OUT/prof_$nm.err; exit $rc; }
   return 0
 }
-run c2_qp2048 --n 2048 --m 512 --steps 40 --warmup 4 || exit 1
-run c4_seq --n 2048 --m 512 --instances 8 --steps 20 --warmup 2 || exit 1
-run c4_conc --n 2048 --m 512 --instances 8 --concurrent --steps 20 --warmup 2 || exit 1
-run c3_lp8192 --problem lp --n 8192 --m 2048 --steps 12 --warmup 2 || exit 1
-run c5_socp --problem socp --n 4096 --m 256 --steps 12 --warmup 2 || exit 1
+want() { [ -z "$CFGS" ] || [[ " $CFGS " == *" $1 "* ]]; }
+want c2 && { run c2_qp2048 --n 2048 --m 512 --steps 40 --warmup 4 || exit 1; }
+want c4s && { run c4_seq --n 2048 --m 512 --instances 8 --steps 20 --warmup 2 || exit 1; }
+want c4 && { run c4_conc --n 2048 --m 512 --instances 8 --concurrent --steps 20 --warmup 2 || exit 1; }
+want c3 && { run c3_lp8192 --problem lp --n 8192 --m 2048 --steps 12 --warmup 2 || exit 1; }
+want c5 && { run c5_socp --problem socp --n 4096 --m 256 --steps 12 --warmup 2 || exit 1; }
+exit 0

@@ -24,7 +24,7 @@ a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 4).astype(np.int64)
 a = a[a[:, 1] > 0]
 t0 = a[:, 1].min()
 names = {0: "LA tile", 1: "P(a) diag", 2: "P(a) row<nchd", 3: "P(b) diag", 4: "S tile", 5: "P(a) row", 6: "P(b) row",
-         7: "S sleep@Pa", 8: "S sleep@Pb", 9: "NF fold tile"}
+         7: "S sleep@Pa", 8: "S sleep@Pb", 9: "NF fold tile", 12: "ragged rows", 13: "tail"}
 print(f"block {os.environ.get('IPM_TRACE_BLOCK')} n={n}: {len(a)} workgroups, span {(a[:, 2].max() - t0) / 100:.1f} us")
 for r in sorted(set((a[:, 0] >> 32).tolist())):
     s = a[(a[:, 0] >> 32) == r]

@@ -152,6 +152,42 @@ def test_potrf_ragged_rows(n, ncols, monkeypatch):
         assert ((got[ncols:] - L21).abs().max() / L21.abs().max()).item() < 1e-10
 
 
+@pytest.mark.parametrize("n,ncols", [(8194, 8193), (2050, 2049), (266, 264), (272, 264), (520, 520)])
+def test_potrf_tail_block(n, ncols, monkeypatch):
+    """A last block of <= 8 columns with <= 16 rows from its origin (the bordered phase-1 system:
+    1 column + the right-hand-side row) is finished by a tail workgroup inside the launch before it
+    (IPM_TAIL, default on) instead of a launch of its own: the factor agrees with the own-launch
+    path to fp64 rounding and with torch's Cholesky / triangular solve to 1e-10; a non-positive
+    pivot in the tail columns reports its 1-based column like the diagonal role."""
+    import torch
+    from gpu_util import potrf as P
+    g = torch.Generator(device="cuda").manual_seed(n + 7)
+    M = torch.rand((n + 5, n), dtype=torch.float64, device="cuda", generator=g) - 0.5
+    A = M.T @ M + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IPM_TAIL", mode)
+        H = A.clone()
+        rc, info = P(H, n, n, ncols=ncols)
+        assert rc == 0 and info == 0
+        out[mode] = torch.tril(H.T)[:, :ncols]
+    scale = out["0"].abs().max()
+    assert ((out["1"] - out["0"]).abs().max() / scale).item() < 1e-12
+    L11 = torch.linalg.cholesky(A[:ncols, :ncols])
+    assert ((out["1"][:ncols] - L11).abs().max() / L11.abs().max()).item() < 1e-10
+    if ncols < n:
+        L21 = torch.linalg.solve_triangular(L11, A[ncols:, :ncols].T, upper=False).T
+        assert ((out["1"][ncols:] - L21).abs().max() / L21.abs().max()).item() < 1e-10
+    # the last factored column made indefinite: info = ncols with and without the tail
+    B = A.clone()
+    B[ncols - 1, ncols - 1] = -1.0
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IPM_TAIL", mode)
+        H = B.clone()
+        rc, info = P(H, n, n, ncols=ncols)
+        assert rc == 1 and info == ncols, (mode, rc, info)
+
+
 @pytest.mark.parametrize("n,ncols", [(8194, 8193), (4100, 4100)])
 def test_potrf_split_trailing_tiles(n, ncols, monkeypatch):
     """Trailing tiles of a launch's last round split in two K halves (IPM_SPLIT, default on; the
