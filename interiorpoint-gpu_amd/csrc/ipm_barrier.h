@@ -70,8 +70,19 @@ void dvec_diag_cones(hipStream_t st, int64_t n, int64_t Kd, const double* Ad, co
 void axpy(hipStream_t st, int64_t n, double a, const double* dx, double* x);
 void lincomb(hipStream_t st, int64_t n, double a, const double* u, double b, const double* v, double* out);
 void mul(hipStream_t st, int64_t n, const double* u, const double* v, double sgn, double* out);
+// (zero != null: also zeroes zero[0, nzero) -- the scalar slots of the reduction that follows)
 void dslacks_lin(hipStream_t st, int64_t n, int64_t m, const double* Cdx, bool has_lb, bool has_ub,
-                 const double* dx, const double* dshp, double* ds);
+                 const double* dx, const double* dshp, double* ds, double* zero = nullptr, int nzero = 0);
+// LP / QP / LP-phase-1 gradient pieces in one launch (k_lin_pieces)
+struct LinPieces {
+  int64_t n = 0, m = 0;
+  const double *d = nullptr, *Cx = nullptr, *lb = nullptr, *ub = nullptr, *x = nullptr, *shp = nullptr;
+  const double *c = nullptr, *Px = nullptr, *q = nullptr;
+  double t = 0.0, add = 0.0;
+  bool ph1 = false;
+  double *s = nullptr, *inv = nullptr, *w = nullptr, *go = nullptr, *dvec = nullptr;
+};
+void lin_pieces(hipStream_t st, const LinPieces& a);
 void slack_at(hipStream_t st, int64_t len, const double* s0, const double* ds, double a, double* out);
 void reduce(hipStream_t st, const ReduceBatch& b, int count, double* out);
 

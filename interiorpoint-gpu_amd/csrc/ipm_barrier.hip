@@ -198,11 +198,69 @@ void mul(hipStream_t st, int64_t n, const double* u, const double* v, double sgn
   if (n > 0) hipLaunchKernelGGL(k_mul, dim3(cdiv(n, 256)), dim3(256), 0, st, n, u, v, sgn, out);
 }
 
+// The LP-family gradient pieces at x in one pass (given Cx, and Px for a QP), each value formed
+// exactly as the separate kernels form it: slacks (k_slacks_lin), inv = 1/(s + 1e-15) (k_inv_eps),
+// w = inv^2 over the C rows (k_sq), go (k_objgrad, not in phase 1), and -- when dvec != null --
+// the Hessian's diagonal vector (phase 1: k_dvec of the bound inverses, else k_dvec_inv of the
+// bound slacks) plus `add`.  Thread e: C row e (e < m) and variable e (e < n).
+__global__ void k_lin_pieces(LinPieces a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = a.n, m = a.m, nub = a.ub ? n : 0;
+  const double sh = a.shp ? *a.shp : 0.0;
+  if (e < m) {
+    const double se = a.shp ? (sh + a.d[e]) - a.Cx[e] : a.d[e] - a.Cx[e];
+    a.s[e] = se;
+    const double iv = 1.0 / (se + 1e-15);
+    a.inv[e] = iv;
+    if (a.w) a.w[e] = iv * iv;
+  }
+  if (e < n) {
+    double su = 0.0, sl = 0.0, iu = 0.0, il = 0.0;
+    if (a.ub) {
+      su = a.shp ? (sh + a.ub[e]) - a.x[e] : a.ub[e] - a.x[e];
+      a.s[m + e] = su;
+      iu = 1.0 / (su + 1e-15);
+      a.inv[m + e] = iu;
+    }
+    if (a.lb) {
+      sl = a.shp ? (sh + a.x[e]) - a.lb[e] : a.x[e] - a.lb[e];
+      a.s[m + nub + e] = sl;
+      il = 1.0 / (sl + 1e-15);
+      a.inv[m + nub + e] = il;
+    }
+    if (a.go) {
+      if (a.c) {
+        a.go[e] = a.t * a.c[e];
+      } else {
+        double v = a.Px ? a.Px[e] : 0.0;
+        if (a.q) v = v + a.q[e];
+        a.go[e] = v * a.t;
+      }
+    }
+    if (a.dvec) {
+      double v = 0.0;
+      if (a.ph1) {
+        if (a.lb) v = v + il * il;
+        if (a.ub) v = v + iu * iu;
+      } else {
+        if (a.lb) { const double r = 1.0 / sl; v = v + r * r; }
+        if (a.ub) { const double r = 1.0 / su; v = v + r * r; }
+      }
+      a.dvec[e] = v + a.add;
+    }
+  }
+}
+void lin_pieces(hipStream_t st, const LinPieces& a) {
+  const int64_t tot = std::max(a.m, a.n);
+  if (tot > 0) hipLaunchKernelGGL(k_lin_pieces, dim3(cdiv(tot, 256)), dim3(256), 0, st, a);
+}
+
 // slack directions for the LP family: ds = [dsh - Cdx | dsh - dx | dsh + dx]
 __global__ void k_dslacks_lin(int64_t n, int64_t m, const double* __restrict__ Cdx, bool has_lb, bool has_ub,
                               const double* __restrict__ dx, const double* __restrict__ dshp,
-                              double* __restrict__ ds) {
+                              double* __restrict__ ds, double* __restrict__ zero, int nzero) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (zero && e < nzero) zero[e] = 0.0;   // (the scalar slots of the next reduction: fill() folded in)
   const int64_t nub = has_ub ? n : 0, nlb = has_lb ? n : 0;
   if (e >= m + nub + nlb) return;
   const double dsh = dshp ? *dshp : 0.0;
@@ -213,11 +271,11 @@ __global__ void k_dslacks_lin(int64_t n, int64_t m, const double* __restrict__ C
   ds[e] = dshp ? dsh + v : v;
 }
 void dslacks_lin(hipStream_t st, int64_t n, int64_t m, const double* Cdx, bool has_lb, bool has_ub,
-                 const double* dx, const double* dshp, double* ds) {
-  const int64_t tot = m + (has_ub ? n : 0) + (has_lb ? n : 0);
+                 const double* dx, const double* dshp, double* ds, double* zero, int nzero) {
+  const int64_t tot = std::max<int64_t>(m + (has_ub ? n : 0) + (has_lb ? n : 0), zero ? nzero : 0);
   if (tot > 0)
     hipLaunchKernelGGL(k_dslacks_lin, dim3(cdiv(tot, 256)), dim3(256), 0, st, n, m, Cdx, has_lb, has_ub, dx,
-                       dshp, ds);
+                       dshp, ds, zero, nzero);
 }
 
 // s_out = s0 + a * ds   (a from a device scalar if ap != null)

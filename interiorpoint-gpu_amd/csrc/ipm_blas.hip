@@ -33,13 +33,10 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // GEMV (row-major M):  y = alpha * M x + beta * y        one wave per row
 // =====================================================================================
 template <bool VEC>
-__global__ __launch_bounds__(256) void k_gemv_n(int64_t rows, int64_t cols, double alpha,
-                                                const double* __restrict__ M, int64_t ldm,
-                                                const double* __restrict__ x, double beta,
-                                                double* __restrict__ y) {
+__device__ __forceinline__ void gemv_row(int64_t row, int64_t cols, double alpha, const double* __restrict__ M,
+                                         int64_t ldm, const double* __restrict__ x, double beta,
+                                         double* __restrict__ y) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
   const double* mr = M + row * ldm;
   double acc0 = 0.0, acc1 = 0.0;
   if (VEC) {
@@ -94,11 +91,52 @@ __global__ __launch_bounds__(256) void k_gemv_n(int64_t rows, int64_t cols, doub
   if (lane == 0) y[row] = (beta == 0.0) ? alpha * s : alpha * s + beta * y[row];
 }
 
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gemv_n(int64_t rows, int64_t cols, double alpha,
+                                                const double* __restrict__ M, int64_t ldm,
+                                                const double* __restrict__ x, double beta,
+                                                double* __restrict__ y) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  gemv_row<VEC>(row, cols, alpha, M, ldm, x, beta, y);
+}
+
+// y1 = M1 x (rows r1) and y2 = M2 x (rows r2) in one launch, each row exactly as k_gemv_n computes
+// it (the Newton step's C x and P x: one launch fewer per use)
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gemv_n2(int64_t cols, const double* __restrict__ x, int64_t r1,
+                                                 const double* __restrict__ M1, int64_t ld1, double* __restrict__ y1,
+                                                 int64_t r2, const double* __restrict__ M2, int64_t ld2,
+                                                 double* __restrict__ y2) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row < r1) gemv_row<VEC>(row, cols, 1.0, M1, ld1, x, 0.0, y1);
+  else if (row - r1 < r2) gemv_row<VEC>(row - r1, cols, 1.0, M2, ld2, x, 0.0, y2);
+}
+
+static bool gemv_vec(const double* M, int64_t ldm, const double* x) {
+  return ((ldm & 1) == 0) && ((((uintptr_t)M) & 15) == 0) && ((((uintptr_t)x) & 15) == 0);
+}
+
+void gemv_n2(hipStream_t st, int64_t cols, const double* x, int64_t r1, const double* M1, int64_t ld1, double* y1,
+             int64_t r2, const double* M2, int64_t ld2, double* y2) {
+  if (r1 <= 0 || r2 <= 0 || gemv_vec(M1, ld1, x) != gemv_vec(M2, ld2, x)) {
+    // (mixed alignment: two launches keep each product bitwise what gemv_n gives)
+    gemv_n(st, r1, cols, 1.0, M1, ld1, x, 0.0, y1);
+    gemv_n(st, r2, cols, 1.0, M2, ld2, x, 0.0, y2);
+    return;
+  }
+  dim3 g(cdiv(r1 + r2, 4)), b(256);
+  if (gemv_vec(M1, ld1, x))
+    hipLaunchKernelGGL(k_gemv_n2<true>, g, b, 0, st, cols, x, r1, M1, ld1, y1, r2, M2, ld2, y2);
+  else
+    hipLaunchKernelGGL(k_gemv_n2<false>, g, b, 0, st, cols, x, r1, M1, ld1, y1, r2, M2, ld2, y2);
+}
+
 void gemv_n(hipStream_t st, int64_t rows, int64_t cols, double alpha, const double* M, int64_t ldm,
             const double* x, double beta, double* y) {
   if (rows <= 0) return;
   dim3 g(cdiv(rows, 4)), b(256);
-  bool vec = ((ldm & 1) == 0) && ((((uintptr_t)M) & 15) == 0) && ((((uintptr_t)x) & 15) == 0);
+  const bool vec = gemv_vec(M, ldm, x);
   if (vec)
     hipLaunchKernelGGL(k_gemv_n<true>, g, b, 0, st, rows, cols, alpha, M, ldm, x, beta, y);
   else
@@ -145,6 +183,41 @@ __global__ __launch_bounds__(256) void k_gemv_t_fin(int64_t cols, int64_t nchunk
   y[j] = (beta == 0.0) ? alpha * s : alpha * s + beta * y[j];
 }
 
+// k_gemv_t_fin (alpha 1, beta 0) with the barrier gradient assembled from its column sum in the
+// same thread: ct[j], then g[j] exactly as k_grad_combine forms it
+__global__ __launch_bounds__(256) void k_gemv_t_fin_grad(int64_t cols, int64_t nchunk, const double* __restrict__ part,
+                                                         double* __restrict__ ct, const double* __restrict__ go,
+                                                         const double* __restrict__ blb, const double* __restrict__ bub,
+                                                         bool ct_first, double* __restrict__ g) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  double s = 0.0;
+  int64_t c = 0;
+  for (; c + 8 <= nchunk; c += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = part[(c + q) * cols + j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; c < nchunk; ++c) s += part[c * cols + j];
+  const double ctj = 1.0 * s;
+  ct[j] = ctj;
+  double v;
+  if (ct_first) {
+    v = go ? go[j] : 0.0;
+    v = go ? v + ctj : ctj;
+    if (blb) v = v - blb[j];
+    if (bub) v = v + bub[j];
+  } else {
+    v = go ? go[j] : 0.0;
+    if (blb) v = v - blb[j];
+    if (bub) v = v + bub[j];
+    v = v + ctj;
+  }
+  g[j] = v;
+}
+
 static void gemv_t_plan(int64_t rows, int64_t cols, int64_t* rchunk, int64_t* nchunk) {
   int64_t cb = cdiv(cols, 256);
   int64_t want = std::max<int64_t>(1, 2048 / std::max<int64_t>(cb, 1));
@@ -178,6 +251,25 @@ void gemv_t(hipStream_t st, int64_t rows, int64_t cols, double alpha, const doub
   }
   hipLaunchKernelGGL(k_gemv_t_fin, dim3(cdiv(cols, 256)), dim3(256), 0, st, cols, nc, alpha, part,
                      beta, y);
+}
+
+void gemv_t_grad(hipStream_t st, int64_t rows, int64_t cols, const double* M, int64_t ldm, const double* x,
+                 double* ct, double* part, int64_t part_elems, const double* go, const double* blb,
+                 const double* bub, bool ct_first, double* g) {
+  if (cols <= 0) return;
+  int64_t rc, nc;
+  gemv_t_plan(rows, cols, &rc, &nc);
+  if (rows <= 0) nc = 0;
+  if (nc * cols > part_elems) {
+    rc = std::max<int64_t>(rows, 1);
+    nc = rows > 0 ? 1 : 0;
+  }
+  if (nc > 0) {
+    dim3 gr(cdiv(cols, 256), nc), b(256);
+    hipLaunchKernelGGL(k_gemv_t_part, gr, b, 0, st, rows, cols, rc, M, ldm, x, nullptr, part);
+  }
+  hipLaunchKernelGGL(k_gemv_t_fin_grad, dim3(cdiv(cols, 256)), dim3(256), 0, st, cols, nc, part, ct, go, blb,
+                     bub, ct_first, g);
 }
 
 // =====================================================================================

@@ -40,6 +40,14 @@ void gemv_t(hipStream_t s, int64_t rows, int64_t cols, double alpha, const doubl
             const double* x, const double* w, double beta, double* y, double* partial_ws,
             int64_t partial_ws_elems);
 int64_t gemv_t_ws_elems(int64_t rows, int64_t cols);
+// y1 = M1 x, y2 = M2 x in one launch (bitwise gemv_n's rows; two launches if the alignments differ)
+void gemv_n2(hipStream_t s, int64_t cols, const double* x, int64_t r1, const double* M1, int64_t ld1, double* y1,
+             int64_t r2, const double* M2, int64_t ld2, double* y2);
+// ct = M^T x (gemv_t with alpha 1, beta 0, no weights) and g = the barrier gradient combine of
+// (go, blb, bub, ct) in the same launch as the column sums (bitwise gemv_t + grad_combine)
+void gemv_t_grad(hipStream_t s, int64_t rows, int64_t cols, const double* M, int64_t ldm, const double* x,
+                 double* ct, double* part, int64_t part_elems, const double* go, const double* blb,
+                 const double* bub, bool ct_first, double* g);
 
 // lower triangle (column-major, ldh) of  H = alpha * X^T diag(w) Y + beta * H + tP * P + diag(dvec)
 // X, Y row-major k x n (ld ldx, ldy).  w, P, dvec may be null.  Y may equal X.

@@ -133,6 +133,10 @@ struct ipm_problem {
   int64_t *rowcone_d = nullptr, *dslot_d = nullptr;
   bool use_backup = false;
   bool pieces_valid = false;  // barrier pieces (inv/coef/G) match the current slack state
+  // w = inv^2 and dvec (with hess_add) were formed with the gradient (gradient_at's fused LP-family
+  // path): assemble_hessian skips them while the slack state is unchanged
+  bool hess_pre = false;
+  double hess_add = 0.0;
   double* sws = nullptr;   // KKT SYRK split tail (syrk_split_ws_doubles)
   double* lsw = nullptr;   // least-squares workspace (lstsq_ws_doubles; null when the method never uses it)
 };
@@ -307,6 +311,7 @@ int64_t carve(ipm_problem* pr, char* base) {
 }
 
 inline hipStream_t S(ipm_problem* pr) { return pr->h->stream; }
+
 inline unsigned* trsv_err(ipm_problem* pr) { return reinterpret_cast<unsigned*>(pr->info + RB_INFO_TRSV_ERR); }
 // the Jacobi eigensolver's info (lstsq_sym_factor) goes to its own word: the Cholesky info words
 // keep meaning "factorization failed" (Q9), and a non-converged eigensolve surfaces at the readback
@@ -325,6 +330,7 @@ void compute_slacks(ipm_problem* pr, const double* xp, double* s, double* lhs, d
     cone_slacks(S(pr), pr->sv, pr->Cx, xp, d.lb, d.ub, shp, lhs, rhs, s);
   }
   pr->pieces_valid = false;
+  pr->hess_pre = false;
 }
 
 // f(xp) pieces into scal slots (f0a, f0b): LP c.x ; QP/SOCP x.Px, q.x ; phase 1: s = xp[n].
@@ -442,11 +448,12 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
   }
   SyrkEpi e;
   if (!pr->socp) {
-    if (pr->m > 0) square(st, pr->m, pr->inv, pr->w);
+    const bool pre = pr->hess_pre && pr->hess_add == add && s == pr->s0;
+    if (pr->m > 0 && !pre) square(st, pr->m, pr->inv, pr->w);
     if (pr->ph1) {
-      dvec_sq(st, pr->n, inv_lb(pr), inv_ub(pr), add, pr->dvec);
+      if (!pre) dvec_sq(st, pr->n, inv_lb(pr), inv_ub(pr), add, pr->dvec);
     } else {
-      dvec_inv_sq(st, pr->n, s_lb(pr, s), s_ub(pr, s), add, pr->dvec);
+      if (!pre) dvec_inv_sq(st, pr->n, s_lb(pr, s), s_ub(pr, s), add, pr->dvec);
       if (pr->qp) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     }
     e.dvec = pr->dvec;
@@ -483,6 +490,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
       border(st, pr->n, pr->H, pr->ldh, pr->hxs, pr->scal + SC_SUMINV2);
     }
   }
+  pr->hess_pre = false;   // (the Cholesky overwrites nothing of w / dvec, but a fallback may rebuild H with another add)
   if (pr->ph1 && psd) {
     // corner += 1e-9 (NewtonSolver.py:269-275 adds 1e-9 to the whole (n+1) diagonal); ones[0] == 1
     axpy(st, 1, 1e-9, pr->ones, pr->H + pr->n * pr->ldh + pr->n);
@@ -978,13 +986,20 @@ struct HostTable {
   }
 };
 
-void prep_linesearch_dirs(ipm_problem* pr) {
+// zero_scal: the slack-direction launch also zeroes the scalar slots (enqueue_scalars(.., true)
+// then skips its fill); C dx and P dx share one GEMV launch (LP family)
+void prep_linesearch_dirs(ipm_problem* pr, bool zero_scal = false) {
   const ipm_problem_desc& d = pr->d;
   hipStream_t st = S(pr);
   const double* dsh = pr->ph1 ? pr->dx + pr->n : nullptr;
   if (!pr->socp) {
-    if (pr->m > 0) gemv_n(st, pr->m, pr->n, 1.0, d.C, d.ldc, pr->dx, 0.0, pr->Cdx);
-    dslacks_lin(st, pr->n, pr->m, pr->Cdx, d.lb != nullptr, d.ub != nullptr, pr->dx, dsh, pr->ds);
+    const bool qpP = !pr->lp && !pr->ph1 && d.P;
+    if (pr->m > 0 && qpP) gemv_n2(st, pr->n, pr->dx, pr->m, d.C, d.ldc, pr->Cdx, pr->n, d.P, d.ldp, pr->Pdx);
+    else if (pr->m > 0) gemv_n(st, pr->m, pr->n, 1.0, d.C, d.ldc, pr->dx, 0.0, pr->Cdx);
+    dslacks_lin(st, pr->n, pr->m, pr->Cdx, d.lb != nullptr, d.ub != nullptr, pr->dx, dsh, pr->ds,
+                zero_scal ? pr->scal : nullptr, SC_COUNT);
+    if (qpP && pr->m <= 0) gemv_n(st, pr->n, pr->n, 1.0, d.P, d.ldp, pr->dx, 0.0, pr->Pdx);
+    return;
   } else {
     gemv_n(st, pr->R + pr->K, pr->n, 1.0, d.X, d.ldx, pr->dx, 0.0, pr->Cdx);
     // dlhs: dense rows from X dx; diagonal cones a * dx ; drhs = c_i.dx (0 without c)
@@ -1082,7 +1097,7 @@ double f_at(ipm_problem* pr, const double* sc, double a) {
   return v;
 }
 
-int enqueue_scalars(ipm_problem* pr, const double* x, bool infeasible, const double* v) {
+int enqueue_scalars(ipm_problem* pr, const double* x, bool infeasible, const double* v, bool zeroed = false) {
   const ipm_problem_desc& d = pr->d;
   ReduceBatch rb{};
   int cnt = 0;
@@ -1111,7 +1126,7 @@ int enqueue_scalars(ipm_problem* pr, const double* x, bool infeasible, const dou
     add(pr->Axb, nullptr, pr->p, RED_SUMSQ, SC_R0B);
   }
   (void)v;
-  fill(S(pr), pr->scal, SC_COUNT, 0.0);
+  if (!zeroed) fill(S(pr), pr->scal, SC_COUNT, 0.0);
   reduce(S(pr), rb, cnt, pr->scal);
   return IPM_OK;
 }
@@ -1334,8 +1349,55 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   return IPM_OK;
 }
 
-// gradient at x with fresh slacks into pr->g (also leaves go, Px, pieces)
-void gradient_at(ipm_problem* pr, const double* x, double t) {
+// gradient at x with fresh slacks into pr->g (also leaves go, Px, pieces).  hess_add >= 0 (the
+// feasible-start loop, LP / QP / LP phase 1 with C rows): the fused path -- C x and P x in one
+// GEMV launch, slacks / inverses / w / go / dvec in one elementwise launch, C^T inv with the
+// gradient combine in its second stage: 4 launches instead of 10, every value bitwise the same
+// (IPM_FUSED_GRAD=0: the separate kernels)
+void gradient_at(ipm_problem* pr, const double* x, double t, double hess_add = -1.0) {
+  const char* efg = getenv("IPM_FUSED_GRAD");   // (read per call: a test compares both paths)
+  const bool fused_on = !(efg && efg[0] == '0');
+  const ipm_problem_desc& d = pr->d;
+  if (fused_on && hess_add >= 0.0 && !pr->socp && pr->m > 0 && !pr->diag) {
+    hipStream_t st = S(pr);
+    const bool qpP = !pr->ph1 && !pr->lp && d.P;
+    if (qpP) gemv_n2(st, pr->n, x, pr->m, d.C, d.ldc, pr->Cx, pr->n, d.P, d.ldp, pr->Px);
+    else gemv_n(st, pr->m, pr->n, 1.0, d.C, d.ldc, x, 0.0, pr->Cx);
+    LinPieces a;
+    a.n = pr->n;
+    a.m = pr->m;
+    a.d = d.d;
+    a.Cx = pr->Cx;
+    a.lb = d.lb;
+    a.ub = d.ub;
+    a.x = x;
+    a.shp = pr->ph1 ? x + pr->n : nullptr;
+    a.t = t;
+    a.ph1 = pr->ph1;
+    a.s = pr->s0;
+    a.inv = pr->inv;
+    a.w = pr->w;
+    if (!pr->ph1) {
+      a.go = pr->go;
+      if (pr->lp) a.c = d.c;
+      else { a.Px = d.P ? pr->Px : nullptr; a.q = d.q; }
+    }
+    a.dvec = pr->dvec;
+    a.add = hess_add;
+    lin_pieces(st, a);
+    gemv_t_grad(st, pr->m, pr->n, d.C, d.ldc, pr->inv, pr->ct, pr->part, pr->part_elems, pr->ph1 ? nullptr : pr->go,
+                inv_lb(pr), inv_ub(pr), pr->ph1, pr->g);
+    if (pr->ph1) {
+      ReduceBatch rb{};
+      rb.ops[0] = ReduceOp{pr->inv, nullptr, pr->Sbar, 1, 1, RED_SUM, SC_SUMINV};
+      reduce(st, rb, 1, pr->scal);
+      t_minus(st, t, pr->scal + SC_SUMINV, pr->g + pr->n);
+    }
+    pr->pieces_valid = true;
+    pr->hess_pre = true;
+    pr->hess_add = hess_add;
+    return;
+  }
   compute_slacks(pr, x, pr->s0, pr->lhs0, pr->rhs0);
   objective_grad(pr, x, t);
   barrier_pieces(pr, pr->s0, pr->lhs0, pr->rhs0);
@@ -1385,13 +1447,14 @@ extern "C" int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v,
   };
 
   for (it = 0; it < o->max_iters; ++it) {
-    gradient_at(pr, x, t);
+    gradient_at(pr, x, t, pr->eq ? -1.0 : (o->use_psd_condition != 0 ? 1e-9 : 0.0));
     if (!pr->eq) {
       // ------------------------------------------------ feasible start (NewtonSolver.py)
       int rc = direction_feasible(pr, t, o);
       if (rc) return bail(rc);
-      prep_linesearch_dirs(pr);
-      enqueue_scalars(pr, x, false, nullptr);
+      const bool zs = !pr->socp;
+      prep_linesearch_dirs(pr, zs);
+      enqueue_scalars(pr, x, false, nullptr, zs);
       int64_t k0 = 0;
       candidate_pass(pr, x, tab.alpha[0], o->beta);
       rc = readback(pr, rb, true);

@@ -144,6 +144,25 @@ EXACT_CASES = sorted(k for k, v in SOLVE_CASES.items() if v != "SOCP" and not k.
 
 
 @pytest.mark.parametrize("name", EXACT_CASES)
+def test_fused_gradient_path_is_bitwise(name, monkeypatch):
+    """The feasible-start gradient in 4 launches (C x and P x in one GEMV launch, slacks / inverses
+    / w / go / dvec in one elementwise launch, C^T inv with the gradient combine in its second
+    stage; C dx and P dx likewise, the scalar slots zeroed by the slack-direction launch) against
+    the separate kernels (IPM_FUSED_GRAD=0): the same iterations, steps and x*, bit for bit."""
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("IPM_FUSED_GRAD", mode)
+        z, s, v = _run(name)
+        steps = [t[0] for t in ((s.phase1_solver.phase1_ns.trace if len(z["phase1_inner_iters"]) else [])
+                                + s.ns.trace)]
+        out[mode] = (list(s.inner_iters), np.array(steps), np.asarray(s.xstar, float).copy(), v)
+    assert out["0"][0] == out["1"][0]
+    np.testing.assert_array_equal(out["0"][1], out["1"][1])
+    np.testing.assert_array_equal(out["0"][2], out["1"][2])
+    assert out["0"][3] == out["1"][3]
+
+
+@pytest.mark.parametrize("name", EXACT_CASES)
 def test_full_solve_reference_exact_linesearch(name, monkeypatch):
     """IPM_LINESEARCH=exact (every trial point formed, fresh slacks by GEMV, f evaluated directly,
     NewtonSolver.py:165-206 step by step): the same bars as the default table replay."""
