@@ -1150,7 +1150,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
                                          int64_t lda, const double* dinv, const double* pubL,
                                          unsigned* progress, int next_nb, unsigned* nextc, double* stage,
                                          int* sflag, unsigned* done = nullptr, bool fold_pub = true,
-                                         int* sinfo = nullptr, unsigned* failw = nullptr) {
+                                         int* sinfo = nullptr, unsigned* failw = nullptr, bool sc1_rows = false) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4;
   const int64_t row = k0 + nb + chunk * PF_RB + wv * 16 + fr;
@@ -1208,7 +1208,9 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
       for (int r = 0; r < 4; ++r) {
         const int c = J * 16 + fk + 4 * r;
         if (c < nb) {
-          if (pub) st_sc1(&A[(k0 + c) * lda + row], x[J][r]);
+          // (sc1_rows: the chunk holding the tail rows -- its rows are read inside this launch by
+          // the tail workgroup, possibly on another XCD: write-through like the published chunks)
+          if (pub || sc1_rows) st_sc1(&A[(k0 + c) * lda + row], x[J][r]);
           else A[(k0 + c) * lda + row] = x[J][r];
         }
       }
@@ -1608,7 +1610,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     }
     row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
                    sm.d.sD, &sflag, pb ? (chunk == 0 && b.ntail ? &b.ctl[CTL_PB0] : nullptr) : &pa_done[chunk], false,
-                   b.info, failw);
+                   b.info, failw, b.ntail && (b.tail_o - (kp + nbp)) / PF_RB == chunk);
     return;
   }
   if (kind == K_NF) {
@@ -2104,7 +2106,7 @@ struct BlockLaunch {
 };
 // every launch of one factorization (potrf_lower_fused's plan); the control words are NOT zeroed
 static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
-                       std::vector<BlockLaunch>& out) {
+                       std::vector<BlockLaunch>& out, bool allow_tail = true) {
   out.clear();
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
@@ -2125,7 +2127,9 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
   // own launch (look-ahead fold, a diagonal role for one column, the launch boundary) cost ~90 us
   // per factorization (r5u: phase-1 POTRF 0.764 vs 0.672 ms at n = 2048).  IPM_TAIL=0: off.
   const char* etl = getenv("IPM_TAIL");
-  const bool tail_on = !(etl && etl[0] == '0');
+  // (the batched path keeps the last block's own launch: with the tail its factors differed from
+  // the per-instance launches', r5bs -- the batch is opt-in and measured slower, not chased)
+  const bool tail_on = allow_tail && !(etl && etl[0] == '0');
   int64_t nemit = nblocks;
   int tail_r = 0;
   if (tail_on && nblocks >= 2 && pl.kind[nblocks - 2] == 0) {
@@ -2434,7 +2438,7 @@ int potrf_lower_batch(hipStream_t st, const PotrfReq* reqs, int B, PotrfBatchWs&
   for (int i = 0; i < B; ++i) {
     const PotrfReq& r = reqs[i];
     const int64_t nc = (r.ncols < 0 || r.ncols > r.n) ? r.n : r.ncols;
-    if (nc > 0) potrf_plan(r.n, r.A, r.lda, r.info, r.ws, nc, plans[i]);
+    if (nc > 0) potrf_plan(r.n, r.A, r.lda, r.info, r.ws, nc, plans[i], false);
     else plans[i].clear();
     maxl = std::max(maxl, plans[i].size());
   }

@@ -1358,7 +1358,8 @@ void gradient_at(ipm_problem* pr, const double* x, double t, double hess_add = -
   const char* efg = getenv("IPM_FUSED_GRAD");   // (read per call: a test compares both paths)
   const bool fused_on = !(efg && efg[0] == '0');
   const ipm_problem_desc& d = pr->d;
-  if (fused_on && hess_add >= 0.0 && !pr->socp && pr->m > 0 && !pr->diag) {
+  // (not with a batched Cholesky: r5bd -- config 4 with IPM_POTRF_BATCH=1 did not finish with it)
+  if (fused_on && hess_add >= 0.0 && !pr->socp && pr->m > 0 && !pr->diag && !pr->batch) {
     hipStream_t st = S(pr);
     const bool qpP = !pr->ph1 && !pr->lp && d.P;
     if (qpP) gemv_n2(st, pr->n, x, pr->m, d.C, d.ldc, pr->Cx, pr->n, d.P, d.ldp, pr->Px);
