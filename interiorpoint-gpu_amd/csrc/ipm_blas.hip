@@ -300,7 +300,7 @@ static void syrk_launch(hipStream_t st, int64_t n, int64_t k, double alpha, cons
   a.dvec = e.dvec;
   a.info = info;
   a.tri = 1;
-  if (e.split_ws) mfma_gemm_launch_split(st, a, e.split_ws, e.split_cap, 2 * num_cus());
+  if (e.split_ws) mfma_gemm_launch_split(st, a, e.split_ws, e.split_cap, 2 * num_cus(), e.flags_zero && !info);
   else mfma_gemm_launch(st, a);
 }
 
@@ -552,6 +552,9 @@ struct DiagSmem {
 // published stores at the end of an iteration (progress J+1 needs block row J: tiles from leaves
 // < J and the diagonal block stored by wave 2 in iteration J+1, never the current leaf's rows);
 // bit 1 -- branch-free LDS loads / stores around the leaf (clamped addresses + selects).
+#ifndef IPM_STEP1_PAIR
+#define IPM_STEP1_PAIR 1
+#endif
 #ifndef IPM_FOLD_ACC
 #define IPM_FOLD_ACC 1
 #endif
@@ -657,6 +660,30 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
     for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) sD[cb + 64 * r] = acc[r];
+  };
+  // two tiles T_{I1,K}, T_{I2,K} -= L_{I,P} L_KP^T at once: the shared L_KP operand loaded once and
+  // the two 4-MFMA chains interleaved (each tile's operations exactly tile_update's)
+  auto tile_update2 = [&](int I1, int I2, int K, int P) {
+    const int o = fk * 16 + fr;
+    const int c1 = bidx(I1, K) * 256 + o, c2 = bidx(I2, K) * 256 + o;
+    const int ab = bidx(K, P) * 256 + o, b1 = bidx(I1, P) * 256 + o, b2 = bidx(I2, P) * 256 + o;
+    dbl4 x1, x2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { x1[r] = sD[c1 + 64 * r]; x2[r] = sD[c2 + 64 * r]; }
+    double av[4], v1[4], v2[4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      av[s4] = -sD[ab + 64 * s4];
+      v1[s4] = sD[b1 + 64 * s4];
+      v2[s4] = sD[b2 + 64 * s4];
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], v1[s4], x1, 0, 0, 0);
+      x2 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], v2[s4], x2, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { sD[c1 + 64 * r] = x1[r]; sD[c2 + 64 * r] = x2[r]; }
   };
   // T_IK -= sum_{P < np} L_IP L_KP^T (two accumulators)
   auto tile_update_n = [&](int I, int K, int np) {
@@ -764,6 +791,11 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   for (int J = 0; J < nJ; ++J) {
     // ---- 1. term J-1 on block column J: wave 0 the diagonal tile, waves 1-3 the tiles below
     if (J > 0) {
+#if IPM_STEP1_PAIR
+      // waves 1-3 with two tiles below run them as one interleaved pair
+      if (wv > 0 && wv + 3 < 8 - J) tile_update2(J + wv, J + wv + 3, J, J - 1);
+      else
+#endif
       for (int tI = (wv == 0 ? 0 : wv); tI < 8 - J; tI += (wv == 0 ? 8 : 3)) tile_update(J + tI, J, J - 1);
       __syncthreads();   // the leaf waves read tiles other waves updated
     }
@@ -1949,6 +1981,17 @@ __global__ void k_zero2(unsigned* a, int64_t na, unsigned* b, int64_t nb) {
   if (i < na) a[i] = 0u;
   else if (i - na < nb) b[i - na] = 0u;
 }
+// k_zero2 plus the bordered right-hand side (k_border_rhs's row N and corner) in the same launch
+__global__ void k_zero2_border(unsigned* a, int64_t na, unsigned* b, int64_t nb, BorderJob j) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < na) a[i] = 0u;
+  else if (i - na < nb) b[i - na] = 0u;
+  else {
+    const int64_t c = i - na - nb;
+    if (c < j.N) j.H[c * j.ldh + j.N] = j.scale * j.g[c];
+    else if (c == j.N) j.H[j.N * j.ldh + j.N] = j.corner;
+  }
+}
 static void zero2(hipStream_t st, void* a, int64_t na, void* b, int64_t nb) {
   const int64_t tot = na + nb;
   if (tot > 0)
@@ -2396,8 +2439,10 @@ static void launch_block(hipStream_t st, const BlockLaunch& L) {
   }
 }
 
-void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols) {
+void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
+                       const BorderJob* border) {
   if (ncols < 0 || ncols > n) ncols = n;
+  if (border && ncols <= 0) border_rhs(st, border->N, border->H, border->ldh, border->g, border->scale);
   if (ncols <= 0) {
     hipMemsetAsync(info, 0, sizeof(int), st);
     return;
@@ -2406,7 +2451,13 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
   potrf_plan(n, A, lda, info, ws, ncols, plan);
   // info, then word 0..7: the "previous launch" of launch 0 (never failed); then cw words per launch
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
-  zero2(st, info, 1, ctl0, 8 + (int64_t)plan.size() * block_ctl_words(n));
+  if (border) {
+    const int64_t nz = 8 + (int64_t)plan.size() * block_ctl_words(n), tot = 1 + nz + border->N + 1;
+    hipLaunchKernelGGL(k_zero2_border, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, st, reinterpret_cast<unsigned*>(info),
+                       (int64_t)1, ctl0, nz, *border);
+  } else {
+    zero2(st, info, 1, ctl0, 8 + (int64_t)plan.size() * block_ctl_words(n));
+  }
   for (const BlockLaunch& L : plan) launch_block(st, L);
 }
 

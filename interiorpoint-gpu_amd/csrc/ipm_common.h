@@ -60,6 +60,9 @@ struct SyrkEpi {
   // null: the plain tile grid
   double* split_ws = nullptr;
   int64_t split_cap = 0;
+  // the flag area is zero on entry (zeroed once when the workspace was carved): the kernels leave
+  // it zero (the last piece / the consuming K half resets its word), so no memset per call
+  bool flags_zero = false;
 };
 // workspace of the split tail for an n x n lower-triangle SYRK: the cap and its size in doubles
 inline int64_t syrk_split_cap(int64_t n) {
@@ -106,8 +109,16 @@ void potrf_lower(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev
 // Blocked right-looking Cholesky, one launch per 256-column block on stream s (k_potrf_block).
 // ncols < n: only the first ncols columns are factored (all n rows) -- the bordered Newton system
 // needs row n-1 of L (the forward-solved right-hand side) but not its diagonal entry.
+// the bordered right-hand side (border_rhs's row N = scale * g, corner) written by the launch
+// that zeroes the control words (one launch fewer per Newton step)
+struct BorderJob {
+  int64_t N = 0, ldh = 0;
+  double* H = nullptr;
+  const double* g = nullptr;
+  double scale = -1.0, corner = 1e300;
+};
 void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws,
-                       int64_t ncols = -1);
+                       int64_t ncols = -1, const BorderJob* border = nullptr);
 // Several independent factorizations in lockstep on stream s (config 4): each request is exactly
 // one potrf_lower_fused call (its own matrix, info word and workspace, ncols as there); block
 // column bk of every request runs in ONE launch (k_potrf_batch), and every request's result is

@@ -189,12 +189,13 @@ void derive(ipm_problem* pr) {
 
 // the Newton step's Cholesky (potrf_lower_fused) -- through the problem's batch when it has one
 static int potrf_step(ipm_problem* pr, hipStream_t st, int64_t n, double* H, int64_t ldh, int* info, double* ws,
-                      int64_t ncols) {
+                      int64_t ncols, const BorderJob* border = nullptr) {
   ipm_potrf_batch* b = pr->batch;
   if (!b) {
-    potrf_lower_fused(st, n, H, ldh, info, ws, ncols);
+    potrf_lower_fused(st, n, H, ldh, info, ws, ncols, border);
     return IPM_OK;
   }
+  if (border) border_rhs(st, border->N, border->H, border->ldh, border->g, border->scale);
   if (!pr->batch_ready && hipEventCreateWithFlags(&pr->batch_ready, hipEventDisableTiming) != hipSuccess)
     return IPM_HIP_ERROR;
   hipEventRecord(pr->batch_ready, st);
@@ -457,7 +458,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
       if (pr->qp) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     }
     e.dvec = pr->dvec;
-    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
+    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); e.flags_zero = true; }
     syrk_lower(st, pr->n, pr->m, 1.0, d.C, d.ldc, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // border: hxs = -C^T inv_C^2 + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (+psd)
@@ -477,7 +478,7 @@ void assemble_hessian(ipm_problem* pr, double t, const double* s, bool psd) {
     if (d.Kd > 0) dvec_diag_cones(st, pr->n, d.Kd, d.Ad, d.dcone_id, pr->coef, pr->dvec);
     if (d.P && !pr->ph1) { e.P = d.P; e.ldp = d.ldp; e.tP = t; }
     e.dvec = pr->dvec;
-    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); }
+    if (pr->sws) { e.split_ws = pr->sws; e.split_cap = syrk_split_cap(pr->n); e.flags_zero = true; }
     syrk_lower(st, pr->n, pr->XR, 1.0, d.X, d.ldx, nullptr, 0, pr->w, 0.0, pr->H, pr->ldh, e);
     if (pr->ph1) {
       // hxs = -sum_i G_i inv_i + inv_lb^2 - inv_ub^2 ; hss = sum inv^2 (barrier segment)
@@ -798,6 +799,11 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
   }
   carve(pr, reinterpret_cast<char*>(workspace));
   hipMemsetAsync(pr->info, 0, RB_MASK, h->stream);   // info words incl. the sticky device error word
+  if (pr->sws) {   // the KKT SYRK's split / stream-K flags: zeroed once, left zero by the kernels
+    const int64_t cap = syrk_split_cap(pr->n);
+    hipMemsetAsync(pr->sws + cap * 128 * 128, 0, (syrk_split_ws_doubles(pr->n) - cap * 128 * 128) * sizeof(double),
+                   h->stream);
+  }
   pr->use_backup = d.solve_method == IPM_SOLVE_LU || d.solve_method == IPM_SOLVE_LSTSQ;
   if (pr->socp) {
     // host-side structure: row -> cone, cone -> diagonal slot
@@ -1156,11 +1162,17 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
     // Cholesky of the bordered [[H, -g], [-g^T, big]]: its last row is y = L^-1 (-g) (the forward
     // solve of NewtonSolver.py:287-299 / cho_solve), then one backward solve L^T dx = y
     ipm_handle* h = pr->h;
-    border_rhs(st, pr->N, pr->H, pr->ldh, pr->g, -1.0);
     if (h->timing) { hipEventRecord(h->ev[2], st); h->potrf_pending = true; }
-    // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side)
+    // bordered: columns 0..N-1 only (row N of L is the forward-solved right-hand side); the row
+    // N = -g itself is written by the launch that zeroes the factorization's control words
     {
-      const int rcb = potrf_step(pr, st, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N);
+      BorderJob bj;
+      bj.N = pr->N;
+      bj.H = pr->H;
+      bj.ldh = pr->ldh;
+      bj.g = pr->g;
+      bj.scale = -1.0;
+      const int rcb = potrf_step(pr, st, pr->N + 1, pr->H, pr->ldh, pr->info, pr->pws, pr->N, &bj);
       if (rcb) return rcb;
     }
     if (h->timing) hipEventRecord(h->ev[3], st);

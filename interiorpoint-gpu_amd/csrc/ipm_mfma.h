@@ -537,6 +537,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     __syncthreads();
     if (tid == 0) __hip_atomic_store(pflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (SPLIT == 2) {
+    // the partial is consumed (its loads fed the stores above): the flag goes back to zero
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(pflag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #ifdef IPM_TILE_STAMPS
   IPM_TSTAMP(3);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -704,6 +709,8 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
       *cp = v;
     }
   }
+  // every piece of this tile has counted: the counter goes back to zero for the next launch
+  if (tid == 0) __hip_atomic_store(&cnt[ti], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // stream-K plan for nt 128-tiles on `slots` slots: pieces per tile P (0: not worth it) and the
@@ -802,7 +809,8 @@ inline void mfma_gemm_launch(hipStream_t st, GemmArgs a) {
 
 // the KKT SYRK with its tail split (ws: cap * BM * BM doubles of partial tiles, then cap flags);
 // falls back to the plain launch when nothing is worth splitting
-inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64_t cap, int slots) {
+inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64_t cap, int slots,
+                                   bool flags_zero = false) {
   if (a.ni <= 0 || a.nj <= 0) return;
   const bool vec = ((a.ldx & 1) == 0) && ((a.ldy & 1) == 0) && ((((uintptr_t)a.X) & 15) == 0) &&
                    ((((uintptr_t)a.Y) & 15) == 0);
@@ -826,7 +834,7 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
       // counters: qk tile words, then npc per-piece words (ws has cap * 128 * 128 doubles of
       // partials, then the flag area)
       unsigned* cnt = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
-      hipMemsetAsync(cnt, 0, (qk + npc) * sizeof(unsigned), st);
+      if (!flags_zero) hipMemsetAsync(cnt, 0, qk * sizeof(unsigned), st);   // (per-piece words: never waited on)
       dim3 g((unsigned)(npc + s_full)), blk(256);
       const int pl = streamk_mode(a.nblk, slots) == 2 ? 1 : 0;
       if (a.w) {
@@ -848,7 +856,7 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
   }
   const int64_t s_full = a.nblk - q;
   unsigned* flags = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
-  hipMemsetAsync(flags, 0, q * sizeof(unsigned), st);
+  if (!flags_zero) hipMemsetAsync(flags, 0, q * sizeof(unsigned), st);
   dim3 g((unsigned)(s_full + 2 * q)), b(256);
 #define IPM_SPLIT_LAUNCH(BMv)                                                                             \
   do {                                                                                                    \
