@@ -901,8 +901,9 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       double dv = rsqrt_pivot(piv);
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        if (V & 65536) dsum += dv;
-        else if (!(piv > 0.0) && bad == 0) bad = c + 1;
+        if (V & 65536) {
+          // (the failure test's sum is formed after the sweep, as a tree)
+        } else if (!(piv > 0.0) && bad == 0) bad = c + 1;
         dvs[c] = dv;
         double pivn = 1.0, dvn = 1.0;
         if (c + 1 < 16) {
@@ -997,9 +998,19 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 #pragma unroll
           for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = row[c];   // column-major
         }
-        if (lane == 0) {
+        if (lane == 0 && !DL) {   // (Dinv from the leaf needs no pivot factors in LDS)
 #pragma unroll
           for (int c = 0; c < 16; ++c) srinv[J * 16 + c] = dvs[c];
+        }
+        // the 16 pivot factors summed as a tree (4 dependent adds instead of 16 on the leaf's tail):
+        // NaN for any pivot <= 0 or NaN, like the running sum, and nothing else reads it
+        {
+          double t8[8], t4[4];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) t8[c] = dvs[2 * c] + dvs[2 * c + 1];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) t4[c] = t8[2 * c] + t8[2 * c + 1];
+          dsum = (t4[0] + t4[1]) + (t4[2] + t4[3]);
         }
         if (!(dsum < __builtin_inf())) {   // a pivot <= 0 or NaN (LAPACK potrf's test), rare
 #pragma unroll
