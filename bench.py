@@ -82,6 +82,16 @@ def trailing_bytes(N, nb=256):
     return tot
 
 
+def potrf_launches(N, nb=256):
+    """k_potrf_block launches of one factorization of the N-column Newton matrix (N + 1 rows with
+    the bordered right-hand side): one per 256-column block, except that a last block of <= 8
+    columns with <= 16 rows below its origin is finished by the launch before it (potrf_plan's
+    tail workgroup; the phase-1 system N = n + 1)."""
+    blocks = math.ceil(N / nb)
+    cbl = (blocks - 1) * nb
+    return blocks - 1 if blocks >= 2 and N - cbl <= 8 and N + 1 - cbl <= 16 else blocks
+
+
 def potrf_flops(N):
     """Cholesky of the N x N Newton matrix (the bordered right-hand side row adds O(N^2))."""
     return N ** 3 / 3 + N ** 2 / 2 + N / 6
@@ -411,7 +421,7 @@ def main():
         tot0 = max(sum(it0.values()), 1.0)
         pf_tot = sum(it0[nm] * potrf_flops(res[nm]["N"]) for nm, _ in segs if it0[nm])
         pt_tot = sum(it0[nm] * per[nm]["potrf_ms"] for nm, _ in segs)
-        launches = sum(it0[nm] * math.ceil(res[nm]["N"] / 256) for nm, _ in segs)
+        launches = sum(it0[nm] * potrf_launches(res[nm]["N"]) for nm, _ in segs)
         kf_tot = sum(it0[nm] * res[nm]["kkt_flops"] for nm, _ in segs)
         kt_tot = sum(it0[nm] * per[nm]["kkt_ms"] for nm, _ in segs)
         potrf_tf = pf_tot / (pt_tot * 1e-3) / 1e12 if pt_tot > 0 else 0.0
@@ -449,7 +459,7 @@ def main():
                          "launches_per_factorization": launches / tot0,
                          # right-looking blocked Cholesky: each launch reads and writes the lower
                          # trailing matrix once (16 B per element), averaged over the launches
-                         "algorithmic_bytes_per_launch": trailing_bytes(Nmain) / math.ceil(Nmain / 256),
+                         "algorithmic_bytes_per_launch": trailing_bytes(Nmain) / potrf_launches(Nmain),
                          "mfma_counters": (pmc_p or {}).get("mfma")},
             "kkt_syrk": {"kernel": "k_mfma_gemm<128,weighted> (KKT assembly H = [tP +] C^T diag(w) C + diag)",
                          "achieved_tflops": kkt_tf, "frac": kkt_tf / FP64_MFMA_PEAK_TFLOPS,

@@ -165,24 +165,6 @@ int ipm_newton_solve(ipm_problem* pr, double* x, double t, double* v, const ipm_
 int ipm_get_use_backup(ipm_problem* pr);
 int ipm_set_use_backup(ipm_problem* pr, int flag);
 
-/* ---- batched Cholesky across concurrently solved problems (config 4: the reference solves its
-   independent instances one after another, testSolver.py:437-808; here a rank's instances run
-   concurrently, one host thread + stream each, ipm355.dist.Shard).  Problems attached to one
-   batch hand the Cholesky of their Newton steps (NewtonSolver.py:286, 303-313) to it: the
-   factorizations that arrive together (members, or those present when an early arrival's bounded
-   wait runs out) run as ONE launch per 256-column block on the batch's own stream; each result is
-   bitwise that of the problem's own factorization.  Not for problems solved one after another
-   from a single thread (they would only add the wait). */
-typedef struct ipm_potrf_batch ipm_potrf_batch;
-int ipm_potrf_batch_create(int device, ipm_potrf_batch** out);
-int ipm_potrf_batch_destroy(ipm_potrf_batch* b);
-/* delta > 0: that many problems start solving; delta < 0: finished ones leave */
-int ipm_potrf_batch_members(ipm_potrf_batch* b, int delta);
-/* batched launches issued, factorizations they carried (so factorizations / launches = batch size) */
-int ipm_potrf_batch_stats(ipm_potrf_batch* b, double* launches, double* factorizations);
-/* attach (b) or detach (NULL) a problem; b must live on the problem's device */
-int ipm_problem_set_potrf_batch(ipm_problem* pr, ipm_potrf_batch* b);
-
 /* ---- level 1: the oracle protocol (FunctionManager.py:94-195) ---------------- */
 /* update_x(x, update_slacks): the evaluation point becomes x [dev]; slacks are
    recomputed only if update_slacks (Q2) */
@@ -262,9 +244,9 @@ int ipm_debug_lstsq_fail_call(int k);
    so the next ticket's bounded poll of that block runs out (exercises the loud failure).
    Process-wide. */
 int ipm_debug_set_trsv_publish_delay(int ticket);
-/* KKT-SYRK flops of one Newton step of this problem (m n (n+1) in total), split between the
-   up-front SYRK kernel and the k-row slices deferred into the Cholesky launches, where they fill
-   the CUs the panel chain leaves idle (opt-in, IPM_DEFER=1) */
+/* KKT-SYRK flops of one Newton step of this problem (m n (n+1) in total): all of them run in the
+   SYRK kernel (*upfront); *deferred is always 0 (the round-2 deferred-slice experiment was
+   removed; the argument is kept so existing bindings need no change) */
 int ipm_kkt_flops(ipm_problem* pr, double* upfront, double* deferred);
 /* measurement: HIP-event time (ms, averaged over `reps`, on the handle's stream) of the HBM-bound
    kernels of one Newton step on this problem's buffers -- ms[0] the slack GEMV C x, ms[1] the

@@ -1394,6 +1394,7 @@ struct BlockArgs {
   // tail_K) to the corner and factors it
   int ntail = 0, tail_r = 0, tail_R = 0, tail_K = 0;
   int64_t tail_o = 0, tail_k0 = 0;
+  unsigned xf = 0;              // IPM_POTRF_X: experiment bits (A/B builds of one library)
 };
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
 __device__ __forceinline__ unsigned cu_key() {
@@ -1462,7 +1463,7 @@ __device__ unsigned long long ipm_fold_trace[32 * 12];
 // K halves): the tiles read C one MFMA block per slab (mfma_tile LAZYC) instead of a 128 KB burst
 // before the first MFMA
 // The roles of one launch for the workgroup holding launch-local ticket t (see the ticket order
-// below).  Shared by the one-instance kernel (k_potrf_block) and the batched one (k_potrf_batch).
+// below).
 template <bool VEC, bool FASTS, int LAZY>
 __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, BlockSmem& sm, int& sflag) {
   const int tid = threadIdx.x;
@@ -1500,6 +1501,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   const bool la_fold = VEC && t < b.nla32 && (b.la32.K % 128) == 0;
   if (t < b.nla && !la_fold) {
     ROLE(0);
+    if (b.xf & 1) __builtin_amdgcn_s_setprio(2);
     int64_t rb;
     if (t < b.nla32) {
       mfma_tile<32, false, VEC, 2, true>(b.la32, t, sm.g32);
@@ -1642,6 +1644,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   }
   if (kind == K_ROW) {
     ROLE(pb ? 6 : (chunk < nchd ? 2 : 5));
+    if (b.xf & 2) __builtin_amdgcn_s_setprio(2);
     if (pb) {
       // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
       const int64_t r0 = b.wbw + chunk * PF_RB;
@@ -1658,6 +1661,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   }
   if (kind == K_NF) {
     ROLE(frole);
+    if (b.xf & 4) __builtin_amdgcn_s_setprio(2);
     // destination block D (rows / columns fo.., fni x fnj, lower) -= L L^T over the fnp source
     // column passes [fsrc + 128 p, fsrc + 128 p + 128): one 32 x 32 lower tile per workgroup,
     // 16 x 16 per wave.  NF: D = P(b)'s diagonal block, L = P(a)'s rows of it (published by the
@@ -1886,7 +1890,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
     if (tid == 0) {
       const unsigned me = 1u + cu_key();
       int q = -1;
-      for (int i = 0; i < NCRIT && q < 0; ++i)
+      for (int i = 0; i < NCRIT && q < 0 && !(b.xf & 8); ++i)
         if (ld_ctl(&b.ctl[CTL_CRIT + i]) == me) q = i;
       if (q >= 0) {
         ROLE(7);
@@ -1947,40 +1951,6 @@ __global__ __launch_bounds__(256, 2) void k_potrf_block(BlockArgs b_arg) {
   if (threadIdx.x == 0) sticket = (int)atomicAdd(&b.ctl[CTL_TICKET], 1u);
   __syncthreads();
   potrf_block_body<VEC, FASTS, LAZY>(b, __builtin_amdgcn_readfirstlane(sticket), sm, sflag);
-}
-
-// ---- batched launches (config 4: several instances' factorizations in lockstep).  One launch
-// covers block column bk of every instance in the batch group: tab[i] is instance i's BlockArgs
-// (exactly what its own k_potrf_block launch would take), and the workgroups draw ONE ticket
-// sequence ordered role class by role class -- every instance's look-ahead tiles, then every
-// P(a) diagonal role, the critical row chunks, fold tiles, P(b) diagonal roles, ragged rows,
-// trailing tiles, the other row chunks -- so that each instance's critical chain starts as early
-// as in its own launch.  Inside an instance the launch-local tickets keep their order (a
-// workgroup still waits only for lower tickets of its own instance: no deadlock for any
-// residency), and every instance runs its own plan: results are bitwise those of its own launch.
-// dec: [0, K) global start of (class c, instance i) at c * B + i (non-decreasing), [K, 2K) the
-// launch-local ticket of that class's first item; K = POTRF_NCLS * B.
-constexpr int POTRF_NCLS = 10;
-template <bool VEC, bool FASTS = false, int LAZY = 0>
-__global__ __launch_bounds__(256, 2) void k_potrf_batch(const BlockArgs* __restrict__ tab, const int* __restrict__ dec,
-                                                        int B, unsigned* gticket) {
-  __shared__ BlockSmem sm;
-  __shared__ int sticket, sflag;
-  if (threadIdx.x == 0) sticket = (int)atomicAdd(gticket, 1u);
-  __syncthreads();
-  const int T = __builtin_amdgcn_readfirstlane(sticket);
-  // the last class/instance entry whose global start is <= T (empty entries repeat the next start)
-  const int K = POTRF_NCLS * B;
-  int lo = 0, hi = K - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (dec[mid] <= T) lo = mid;
-    else hi = mid - 1;
-  }
-  const int k = __builtin_amdgcn_readfirstlane(lo);
-  const int i = k % B;
-  const int64_t t = (int64_t)dec[K + k] + (T - dec[k]);
-  potrf_block_body<VEC, FASTS, LAZY>(tab[i], t, sm, sflag);
 }
 
 // workspace: [P(a) Dinv + L11][P(b) Dinv + L11][control words]
@@ -2151,16 +2121,15 @@ void set_potrf_spin_limit_us(unsigned us) { set_spin_ticks(0, us); }
 
 // One planned launch of the factorization: its arguments, grid and kernel instantiation
 // (0 <true,true,1> lazy-C, 1 <true,true,2> pair lazy-C, 2 <true,true> fast loop, 3 <true,false>,
-// 4 <false,false>), and the sizes of its ticket classes in ticket order (k_potrf_batch).
+// 4 <false,false>).
 struct BlockLaunch {
   BlockArgs b;
   int64_t grid = 0;
   int inst = 4;
-  int64_t cls[POTRF_NCLS] = {};
 };
 // every launch of one factorization (potrf_lower_fused's plan); the control words are NOT zeroed
 static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws, int64_t ncols,
-                       std::vector<BlockLaunch>& out, bool allow_tail = true) {
+                       std::vector<BlockLaunch>& out) {
   out.clear();
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
@@ -2181,9 +2150,7 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
   // own launch (look-ahead fold, a diagonal role for one column, the launch boundary) cost ~90 us
   // per factorization (r5u: phase-1 POTRF 0.764 vs 0.672 ms at n = 2048).  IPM_TAIL=0: off.
   const char* etl = getenv("IPM_TAIL");
-  // (the batched path keeps the last block's own launch: with the tail its factors differed from
-  // the per-instance launches', r5bs -- the batch is opt-in and measured slower, not chased)
-  const bool tail_on = allow_tail && !(etl && etl[0] == '0');
+  const bool tail_on = !(etl && etl[0] == '0');
   int64_t nemit = nblocks;
   int tail_r = 0;
   if (tail_on && nblocks >= 2 && pl.kind[nblocks - 2] == 0) {
@@ -2380,6 +2347,8 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
       b.trace = bk == tb;
     }
 #endif
+    static const unsigned xf = [] { const char* e = getenv("IPM_POTRF_X"); return e ? (unsigned)strtoul(e, nullptr, 0) : 0u; }();
+    b.xf = xf;
     b.nra = (int)cdiv(std::max<int64_t>(n - cb - b.wa, 0), PF_RB);
     b.nrb = b.wbw > 0 ? (int)cdiv(std::max<int64_t>(n - cb - wb, 0), PF_RB) : 0;
     {
@@ -2430,10 +2399,6 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
     const bool lazy2 = lazy2_on && fasts && b.s.K == 2 * CH_NB && b.nstrip + b.s_full == b.ns &&
                        (b.nstrip == 0 || b.s2.K == 2 * CH_NB) && (b.nrag == 0 || b.rag_K <= 2 * CH_NB);
     L.inst = (vec && lazy) ? 0 : (vec && lazy2) ? 1 : (vec && fasts) ? 2 : vec ? 3 : 4;
-    // ticket classes in launch-local order (potrf_block_body's decode)
-    const int64_t nchd = b.wbw > 0 ? (b.wbw + PF_RB - 1) / PF_RB : 0;
-    const int64_t cls[POTRF_NCLS] = {b.nla, 1, nchd, b.nnf, b.wbw > 0 ? 1 : 0, b.nrag, b.ns, b.nra - nchd, b.nrb, b.ntail};
-    for (int c = 0; c < POTRF_NCLS; ++c) L.cls[c] = cls[c];
     L.b = b;
     out.push_back(L);
   }
@@ -2470,119 +2435,6 @@ void potrf_lower_fused(hipStream_t st, int64_t n, double* A, int64_t lda, int* i
     zero2(st, info, 1, ctl0, 8 + (int64_t)plan.size() * block_ctl_words(n));
   }
   for (const BlockLaunch& L : plan) launch_block(st, L);
-}
-
-// ---- batched factorizations (k_potrf_batch).  Argument tables in device memory, one copy per call
-// from pinned staging: [zero list (B)][ticket counters (launch groups)][per group: BlockArgs x Bg,
-// dec ints x 2 K].  Every instance keeps its own plan, control words and workspace.
-struct ZeroEnt {
-  unsigned* ctl0;
-  int64_t words;
-  int* info;
-};
-__global__ void k_zero_batch(const ZeroEnt* __restrict__ ents, int B, unsigned* counters, int ng) {
-  if ((int)blockIdx.x < B) {
-    const ZeroEnt e = ents[blockIdx.x];
-    for (int64_t i = threadIdx.x; i < e.words; i += blockDim.x) e.ctl0[i] = 0u;
-    if (threadIdx.x == 0 && e.info) *e.info = 0;
-  } else {
-    for (int i = threadIdx.x; i < ng; i += blockDim.x) counters[i] = 0u;
-  }
-}
-
-static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
-
-int potrf_lower_batch(hipStream_t st, const PotrfReq* reqs, int B, PotrfBatchWs& w) {
-  if (B <= 0) return 0;
-  thread_local std::vector<std::vector<BlockLaunch>> plans;
-  plans.resize(B);
-  size_t maxl = 0;
-  for (int i = 0; i < B; ++i) {
-    const PotrfReq& r = reqs[i];
-    const int64_t nc = (r.ncols < 0 || r.ncols > r.n) ? r.n : r.ncols;
-    if (nc > 0) potrf_plan(r.n, r.A, r.lda, r.info, r.ws, nc, plans[i], false);
-    else plans[i].clear();
-    maxl = std::max(maxl, plans[i].size());
-  }
-  // launch groups: block column bk of every instance that has one, split by kernel instantiation
-  struct Group { size_t bk; int inst; std::vector<int> ids; size_t tab_off, dec_off; int64_t grid; };
-  std::vector<Group> groups;
-  for (size_t bk = 0; bk < maxl; ++bk)
-    for (int inst = 0; inst < 5; ++inst) {
-      Group g{bk, inst, {}, 0, 0, 0};
-      for (int i = 0; i < B; ++i)
-        if (plans[i].size() > bk && plans[i][bk].inst == inst) g.ids.push_back(i);
-      if (!g.ids.empty()) groups.push_back(std::move(g));
-    }
-  const int ng = (int)groups.size();
-  size_t off = align_up(sizeof(ZeroEnt) * B, 256);
-  const size_t cnt_off = off;
-  off = align_up(off + sizeof(unsigned) * std::max(ng, 1), 256);
-  for (Group& g : groups) {
-    g.tab_off = off;
-    off = align_up(off + sizeof(BlockArgs) * g.ids.size(), 256);
-    g.dec_off = off;
-    off = align_up(off + sizeof(int) * 2 * POTRF_NCLS * g.ids.size(), 256);
-  }
-  const size_t need = off;
-  if (need > w.bytes) {
-    hipStreamSynchronize(st);   // (the old tables may still be read by queued launches)
-    if (w.dev) hipFree(w.dev);
-    if (w.host) hipHostFree(w.host);
-    w.dev = w.host = nullptr;
-    w.bytes = 0;
-    const size_t sz = std::max<size_t>(need * 2, 1 << 16);
-    if (hipMalloc(&w.dev, sz) != hipSuccess || hipHostMalloc(&w.host, sz) != hipSuccess) return -1;
-    w.bytes = sz;
-  }
-  if (!w.copied) hipEventCreateWithFlags(&w.copied, hipEventDisableTiming);
-  else hipEventSynchronize(w.copied);   // the staging buffer's previous copy has landed
-  char* h = static_cast<char*>(w.host);
-  char* d = static_cast<char*>(w.dev);
-  ZeroEnt* ze = reinterpret_cast<ZeroEnt*>(h);
-  for (int i = 0; i < B; ++i) {
-    ze[i].ctl0 = reinterpret_cast<unsigned*>(reqs[i].ws + 2 * PANEL_WS);
-    ze[i].words = plans[i].empty() ? 0 : 8 + (int64_t)plans[i].size() * block_ctl_words(reqs[i].n);
-    ze[i].info = reqs[i].info;
-  }
-  for (Group& g : groups) {
-    const int Bg = (int)g.ids.size(), K = POTRF_NCLS * Bg;
-    BlockArgs* tab = reinterpret_cast<BlockArgs*>(h + g.tab_off);
-    int* dec = reinterpret_cast<int*>(h + g.dec_off);
-    int64_t gstart = 0;
-    for (int j = 0; j < Bg; ++j) std::memcpy(static_cast<void*>(&tab[j]), &plans[g.ids[j]][g.bk].b, sizeof(BlockArgs));
-    for (int c = 0; c < POTRF_NCLS; ++c)
-      for (int j = 0; j < Bg; ++j) {
-        const BlockLaunch& L = plans[g.ids[j]][g.bk];
-        int64_t lstart = 0;
-        for (int c2 = 0; c2 < c; ++c2) lstart += L.cls[c2];
-        dec[c * Bg + j] = (int)gstart;
-        dec[K + c * Bg + j] = (int)lstart;
-        gstart += L.cls[c];
-      }
-    g.grid = gstart;
-  }
-  if (hipMemcpyAsync(w.dev, w.host, need, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
-  hipEventRecord(w.copied, st);
-  unsigned* counters = reinterpret_cast<unsigned*>(d + cnt_off);
-  hipLaunchKernelGGL(k_zero_batch, dim3((unsigned)B + 1), dim3(256), 0, st, reinterpret_cast<const ZeroEnt*>(d), B,
-                     counters, ng);
-  for (int q = 0; q < ng; ++q) {
-    const Group& g = groups[q];
-    if (g.grid <= 0) continue;
-    const BlockArgs* tab = reinterpret_cast<const BlockArgs*>(d + g.tab_off);
-    const int* dec = reinterpret_cast<const int*>(d + g.dec_off);
-    const dim3 gr((unsigned)g.grid), t(256);
-    const int Bg = (int)g.ids.size();
-    switch (g.inst) {
-      case 0: hipLaunchKernelGGL((k_potrf_batch<true, true, 1>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
-      case 1: hipLaunchKernelGGL((k_potrf_batch<true, true, 2>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
-      case 2: hipLaunchKernelGGL((k_potrf_batch<true, true>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
-      case 3: hipLaunchKernelGGL((k_potrf_batch<true, false>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
-      default: hipLaunchKernelGGL((k_potrf_batch<false, false>), gr, t, 0, st, tab, dec, Bg, counters + q); break;
-    }
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 static int num_cus() {

@@ -119,24 +119,6 @@ struct BorderJob {
 };
 void potrf_lower_fused(hipStream_t s, int64_t n, double* H, int64_t ldh, int* info_dev, double* ws,
                        int64_t ncols = -1, const BorderJob* border = nullptr);
-// Several independent factorizations in lockstep on stream s (config 4): each request is exactly
-// one potrf_lower_fused call (its own matrix, info word and workspace, ncols as there); block
-// column bk of every request runs in ONE launch (k_potrf_batch), and every request's result is
-// bitwise what its own potrf_lower_fused would give.  w: argument-table scratch (grown on demand,
-// owned by the caller).  Returns 0, or -1 on a HIP error.
-struct PotrfReq {
-  int64_t n = 0, lda = 0, ncols = -1;
-  double* A = nullptr;
-  int* info = nullptr;
-  double* ws = nullptr;
-};
-struct PotrfBatchWs {
-  void* dev = nullptr;
-  void* host = nullptr;   // pinned staging
-  size_t bytes = 0;
-  hipEvent_t copied = nullptr;
-};
-int potrf_lower_batch(hipStream_t s, const PotrfReq* reqs, int count, PotrfBatchWs& w);
 // L L^T X = B in place, L column-major lower; B row-major n x nrhs (ldb); W scratch n x nrhs;
 // ctl: 4 device words for the single-RHS persistent solves (null -> blocked multi-RHS path)
 void potrs_lower(hipStream_t s, int64_t n, int64_t nrhs, const double* L, int64_t ldl, double* B,

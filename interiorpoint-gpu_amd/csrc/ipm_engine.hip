@@ -15,13 +15,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cmath>
-#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -60,53 +57,8 @@ enum Slot {
 };
 }  // namespace
 
-// ---- batched Cholesky across concurrent problems (config 4, ipm355.dist.Shard).  Problems solved
-// from several host threads, one stream each, join ONE ipm_potrf_batch.  A problem's Newton step
-// hands its factorization to the batch instead of launching it: the thread records an event on its
-// stream and waits (bounded) for the other members; the last to arrive -- or the first whose wait
-// runs out -- launches every pending factorization together on the batch's own stream
-// (potrf_lower_batch: one launch per 256-column block for all of them) after waiting for each
-// member's event, and every member's stream then waits for the batch's completion event.  The
-// other kernels of a Newton step stay on the member's stream.  Each factorization is bitwise what
-// it would be alone (potrf_lower_batch), so batching changes timing only.
-struct ipm_potrf_batch {
-  int device = 0;
-  hipStream_t exec = nullptr;
-  std::mutex mu;
-  std::condition_variable cv;
-  int members = 0;                 // problems currently solving (join / leave)
-  unsigned wait_us = 400;          // how long an early arrival waits for the others
-  struct Pending { PotrfReq r; hipEvent_t ready; };
-  std::vector<Pending> pending;
-  uint64_t gen = 0;                // batches launched
-  static constexpr int RING = 16;
-  hipEvent_t done[RING] = {};
-  PotrfBatchWs ws;
-  std::vector<PotrfReq> reqs;
-  double launches = 0, factorizations = 0;
-  std::string err;
-  // (mu held) launch everything pending as one batch
-  void launch_locked() {
-    if (pending.empty()) return;
-    reqs.clear();
-    for (const Pending& q : pending) {
-      hipStreamWaitEvent(exec, q.ready, 0);
-      reqs.push_back(q.r);
-    }
-    if (potrf_lower_batch(exec, reqs.data(), (int)reqs.size(), ws) != 0) err = "potrf_lower_batch: HIP error";
-    hipEventRecord(done[gen % RING], exec);
-    launches += 1;
-    factorizations += (double)reqs.size();
-    pending.clear();
-    ++gen;
-    cv.notify_all();
-  }
-};
-
 struct ipm_problem {
   ipm_handle* h = nullptr;
-  ipm_potrf_batch* batch = nullptr;   // batched Cholesky (null: launched on the problem's stream)
-  hipEvent_t batch_ready = nullptr;
   ipm_problem_desc d{};
   // dims / flags
   int64_t n = 0, N = 0, S = 0, Sbar = 0, nub = 0, nlb = 0, m = 0, p = 0, K = 0, R = 0, XR = 0, Lh = 0;
@@ -187,44 +139,12 @@ void derive(ipm_problem* pr) {
   pr->ldh = (pr->N + 1) + ((pr->N + 1) & 1);
 }
 
-// the Newton step's Cholesky (potrf_lower_fused) -- through the problem's batch when it has one
+// the Newton step's Cholesky (potrf_lower_fused on the problem's stream)
 static int potrf_step(ipm_problem* pr, hipStream_t st, int64_t n, double* H, int64_t ldh, int* info, double* ws,
                       int64_t ncols, const BorderJob* border = nullptr) {
-  ipm_potrf_batch* b = pr->batch;
-  if (!b) {
-    potrf_lower_fused(st, n, H, ldh, info, ws, ncols, border);
-    return IPM_OK;
-  }
-  if (border) border_rhs(st, border->N, border->H, border->ldh, border->g, border->scale);
-  if (!pr->batch_ready && hipEventCreateWithFlags(&pr->batch_ready, hipEventDisableTiming) != hipSuccess)
-    return IPM_HIP_ERROR;
-  hipEventRecord(pr->batch_ready, st);
-  PotrfReq r;
-  r.n = n;
-  r.lda = ldh;
-  r.ncols = ncols;
-  r.A = H;
-  r.info = info;
-  r.ws = ws;
-  std::unique_lock<std::mutex> lk(b->mu);
-  b->pending.push_back({r, pr->batch_ready});
-  const uint64_t my = b->gen;
-  if ((int)b->pending.size() >= b->members) {
-    b->launch_locked();
-  } else {
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(b->wait_us);
-    while (b->gen == my) {
-      if (b->cv.wait_until(lk, deadline) == std::cv_status::timeout && b->gen == my) {
-        b->launch_locked();
-        break;
-      }
-    }
-  }
-  hipEvent_t done = b->done[my % ipm_potrf_batch::RING];
-  const bool bad = !b->err.empty();
-  lk.unlock();
-  if (bad) return IPM_HIP_ERROR;
-  return hipStreamWaitEvent(st, done, 0) == hipSuccess ? IPM_OK : IPM_HIP_ERROR;
+  (void)pr;
+  potrf_lower_fused(st, n, H, ldh, info, ws, ncols, border);
+  return IPM_OK;
 }
 
 int64_t carve(ipm_problem* pr, char* base) {
@@ -832,64 +752,7 @@ extern "C" int ipm_problem_create(ipm_handle* h, const ipm_problem_desc* desc, v
 }
 
 extern "C" int ipm_problem_destroy(ipm_problem* pr) {
-  if (pr && pr->batch_ready) hipEventDestroy(pr->batch_ready);
   delete pr;
-  return IPM_OK;
-}
-
-// ---- batched Cholesky (ipm_potrf_batch above)
-extern "C" int ipm_potrf_batch_create(int device, ipm_potrf_batch** out) {
-  if (!out) return IPM_INVALID_ARG;
-  auto* b = new ipm_potrf_batch();
-  b->device = device;
-  int cur = 0;
-  hipGetDevice(&cur);
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->exec, hipStreamNonBlocking) != hipSuccess) {
-    hipSetDevice(cur);
-    delete b;
-    return IPM_HIP_ERROR;
-  }
-  for (auto& e : b->done) hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  if (const char* w = getenv("IPM_BATCH_WAIT_US")) b->wait_us = (unsigned)atoi(w);
-  hipSetDevice(cur);
-  *out = b;
-  return IPM_OK;
-}
-
-extern "C" int ipm_potrf_batch_destroy(ipm_potrf_batch* b) {
-  if (!b) return IPM_OK;
-  hipStreamSynchronize(b->exec);
-  for (auto& e : b->done) if (e) hipEventDestroy(e);
-  if (b->ws.copied) hipEventDestroy(b->ws.copied);
-  if (b->ws.dev) hipFree(b->ws.dev);
-  if (b->ws.host) hipHostFree(b->ws.host);
-  hipStreamDestroy(b->exec);
-  delete b;
-  return IPM_OK;
-}
-
-// delta > 0: problems that start solving join; delta < 0: finished ones leave (a pending batch
-// that no longer waits for anyone is launched)
-extern "C" int ipm_potrf_batch_members(ipm_potrf_batch* b, int delta) {
-  if (!b) return IPM_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(b->mu);
-  b->members = std::max(0, b->members + delta);
-  if (!b->pending.empty() && (int)b->pending.size() >= b->members) b->launch_locked();
-  return b->err.empty() ? IPM_OK : IPM_HIP_ERROR;
-}
-
-extern "C" int ipm_potrf_batch_stats(ipm_potrf_batch* b, double* launches, double* factorizations) {
-  if (!b) return IPM_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(b->mu);
-  if (launches) *launches = b->launches;
-  if (factorizations) *factorizations = b->factorizations;
-  return IPM_OK;
-}
-
-extern "C" int ipm_problem_set_potrf_batch(ipm_problem* pr, ipm_potrf_batch* b) {
-  if (!pr) return IPM_INVALID_ARG;
-  if (b && b->device != pr->h->device) return IPM_INVALID_ARG;
-  pr->batch = b;
   return IPM_OK;
 }
 
@@ -1370,8 +1233,7 @@ void gradient_at(ipm_problem* pr, const double* x, double t, double hess_add = -
   const char* efg = getenv("IPM_FUSED_GRAD");   // (read per call: a test compares both paths)
   const bool fused_on = !(efg && efg[0] == '0');
   const ipm_problem_desc& d = pr->d;
-  // (not with a batched Cholesky: r5bd -- config 4 with IPM_POTRF_BATCH=1 did not finish with it)
-  if (fused_on && hess_add >= 0.0 && !pr->socp && pr->m > 0 && !pr->diag && !pr->batch) {
+  if (fused_on && hess_add >= 0.0 && !pr->socp && pr->m > 0 && !pr->diag) {
     hipStream_t st = S(pr);
     const bool qpP = !pr->ph1 && !pr->lp && d.P;
     if (qpP) gemv_n2(st, pr->n, x, pr->m, d.C, d.ldc, pr->Cx, pr->n, d.P, d.ldp, pr->Px);

@@ -74,11 +74,6 @@ EXPORTS = {
     "ipm_newton_solve": (C.c_int, [P, P, F64, P, C.POINTER(NewtonOpts), C.POINTER(NewtonResult)]),
     "ipm_get_use_backup": (C.c_int, [P]),
     "ipm_set_use_backup": (C.c_int, [P, C.c_int]),
-    "ipm_potrf_batch_create": (C.c_int, [C.c_int, C.POINTER(P)]),
-    "ipm_potrf_batch_destroy": (C.c_int, [P]),
-    "ipm_potrf_batch_members": (C.c_int, [P, C.c_int]),
-    "ipm_potrf_batch_stats": (C.c_int, [P, C.POINTER(F64), C.POINTER(F64)]),
-    "ipm_problem_set_potrf_batch": (C.c_int, [P, P]),
     "ipm_fm_update_x": (C.c_int, [P, P, C.c_int]),
     "ipm_fm_slacks": (C.c_int, [P, P]),
     "ipm_fm_num_slacks": (I64, [P]),
@@ -189,40 +184,6 @@ class Handle:
         if rc == IPM_LINALG_NOT_CONVERGED:
             raise np.linalg.LinAlgError(f"SVD did not converge in Linear Least Squares ({msg})")
         raise IPMBackendError(f"ipm355 error {rc}: {msg}")
-
-
-class PotrfBatch:
-    """ipm_potrf_batch: batched Cholesky for problems solved concurrently on one device (config 4;
-    include/ipm355.h).  Attach problems with DeviceProblem.set_potrf_batch; members(+k / -k) as
-    solving threads start / finish."""
-
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
-        self.device = device
-        h = P()
-        rc = self.lib.ipm_potrf_batch_create(int(device), C.byref(h))
-        if rc != IPM_OK:
-            raise IPMBackendError(f"ipm_potrf_batch_create failed ({rc})")
-        self.ptr = h
-
-    def members(self, delta: int):
-        rc = self.lib.ipm_potrf_batch_members(self.ptr, int(delta))
-        if rc != IPM_OK:
-            raise IPMBackendError(f"batched Cholesky failed ({rc})")
-
-    def stats(self):
-        """(batched launches, factorizations they carried)"""
-        a, b = F64(), F64()
-        self.lib.ipm_potrf_batch_stats(self.ptr, C.byref(a), C.byref(b))
-        return a.value, b.value
-
-    def __del__(self):
-        try:
-            if getattr(self, "ptr", None):
-                self.lib.ipm_potrf_batch_destroy(self.ptr)
-                self.ptr = None
-        except Exception:
-            pass
 
 
 def dptr(t) -> P:

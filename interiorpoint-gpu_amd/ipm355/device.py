@@ -205,7 +205,8 @@ class DeviceProblem:
         return r
 
     def kkt_flops(self):
-        """(up-front SYRK flops, flops of the slices deferred into the Cholesky) per Newton step"""
+        """(KKT SYRK flops per Newton step, 0.0): the second value is the removed deferred-slice
+        split, always 0"""
         a, b = ct.c_double(), ct.c_double()
         self.call(self.handle.lib.ipm_kkt_flops, self.ptr, ct.byref(a), ct.byref(b))
         return a.value, b.value
@@ -221,12 +222,6 @@ class DeviceProblem:
         return {"k_gemv_n (slacks: C x)": (ms[0], 8.0 * (m * n + n + m)),
                 "k_gemv_t_part (gradient: C^T w)": (ms[1], 8.0 * (m * n + m + n)),
                 "k_ls_lin (64 line-search candidates)": (ms[2], 16.0 * S)}
-
-    def set_potrf_batch(self, batch):
-        """Hand this problem's Newton-step Cholesky to a PotrfBatch (None: back to its own stream).
-        The batch must stay alive while the problem uses it."""
-        self._potrf_batch = batch
-        self.check(self.handle.lib.ipm_problem_set_potrf_batch(self.ptr, batch.ptr if batch is not None else None))
 
     @property
     def use_backup(self):

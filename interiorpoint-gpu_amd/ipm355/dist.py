@@ -98,20 +98,11 @@ class Shard:
     streams sharing a queue serialise): call ``configure_queues()`` before anything initialises
     the GPU.  concurrent=False: one after another on the current stream."""
 
-    def __init__(self, make_instance, indices, solver_cls, kwargs=None, device=None, concurrent=False,
-                 batch=None):
+    def __init__(self, make_instance, indices, solver_cls, kwargs=None, device=None, concurrent=False):
         import torch
         self.indices = list(indices)
         self.dev = local_device(device)
         self.concurrent = bool(concurrent)
-        # batched Cholesky (ipm_potrf_batch): the concurrent instances' factorizations run as one
-        # launch per 256-column block.  Opt-in (batch=True or IPM_POTRF_BATCH=1): measured on config 4
-        # (8 x n=2048, r5d) it LOSES -- 1647-1774 Newton it/s against 3107-3122 without it: the
-        # rendezvous puts every instance in lockstep, so the latency-bound small kernels of all
-        # instances run in the same phase instead of filling the gaps of the others' Cholesky chains.
-        if batch is None:
-            batch = self.concurrent and os.environ.get("IPM_POTRF_BATCH", "0") == "1"
-        self.batch = None
         self.streams = ([torch.cuda.Stream(device=torch.device("cuda", self.dev)) for _ in self.indices]
                         if self.concurrent else [None] * len(self.indices))
         self.solvers = []
@@ -122,12 +113,6 @@ class Shard:
             if s.dev.index != self.dev:
                 raise RuntimeError(f"solver placed on {s.dev}, rank owns cuda:{self.dev}")
             self.solvers.append(s)
-        if batch and self.concurrent and len(self.solvers) > 1:
-            from ._lib import PotrfBatch
-            self.batch = PotrfBatch(self.dev)
-            for s in self.solvers:
-                for prob in _device_problems(s):
-                    prob.set_potrf_batch(self.batch)
 
     def solve(self, **solve_kwargs):
         """Solve every instance (solve_kwargs go to each solver's solve(), e.g. iteration_budget);
@@ -156,13 +141,7 @@ class Shard:
                 groups.setdefault(st.cuda_stream, []).append(k)
 
             def run_group(ks):
-                try:
-                    return [one(k) for k in ks]
-                finally:
-                    if self.batch is not None:
-                        self.batch.members(-1)      # this thread solves no more: stop waiting for it
-            if self.batch is not None:
-                self.batch.members(len(groups))
+                return [one(k) for k in ks]
             with ThreadPoolExecutor(max_workers=len(groups)) as ex:
                 out = dict(r for rs in ex.map(run_group, list(groups.values())) for r in rs)
         else:
@@ -173,20 +152,6 @@ class Shard:
 
     def xstar(self):
         return {i: s.xstar for i, s in zip(self.indices, self.solvers)}
-
-
-def _device_problems(solver):
-    """The DeviceProblems a solver's Newton steps run on: its barrier problem and, when it has one,
-    its phase-1 problem."""
-    out = []
-    fm = getattr(solver, "fm", None)
-    if fm is not None and getattr(fm, "prob", None) is not None:
-        out.append(fm.prob)
-    p1 = getattr(solver, "phase1_solver", None)
-    fm1 = getattr(p1, "phase1_fm", None) if p1 is not None else None
-    if fm1 is not None and getattr(fm1, "prob", None) is not None:
-        out.append(fm1.prob)
-    return out
 
 
 def _on(stream):

@@ -161,7 +161,7 @@ def test_shard_concurrent_groups_instances_by_stream():
             return float(self.sid)
 
     sh = object.__new__(D.Shard)
-    sh.indices, sh.dev, sh.concurrent, sh.batch = list(range(40)), 0, True, None
+    sh.indices, sh.dev, sh.concurrent = list(range(40)), 0, True
     sh.streams = [FakeStream(i % 32) for i in range(40)]
     sh.solvers = [FakeSolver(i % 32) for i in range(40)]
     out = sh.solve()

@@ -252,40 +252,6 @@ def test_m4_shard_on_one_gpu(concurrent):
             assert int(tab[i, 1]) == ref_iters
 
 
-@pytest.mark.skipif(os.environ.get("IPM_TEST_BATCH") != "1",
-                    reason="the opt-in batched Cholesky (IPM_POTRF_BATCH=1) is timing-dependent on this pool: "
-                           "the same library passed in 8 s and hung past 140 s on two boxes (profiles/r5b3); "
-                           "IPM_TEST_BATCH=1 runs it")
-def test_m4_shard_batched_cholesky_bitwise(monkeypatch):
-    """The batched Cholesky of config 4 (ipm_potrf_batch, one k_potrf_batch
-    launch per 256-column block for every concurrently solving instance) changes timing only: the
-    eight M4 instances solved concurrently WITH the batch and WITHOUT it (IPM_POTRF_BATCH=0 path,
-    batch=False) give bitwise the same x* and iteration counts, the batch really carried several
-    factorizations per launch, and phase 1 (bordered n+1 systems) and the barrier phase (n) mixed
-    in one batch are fine."""
-    from ipm355 import dist
-    from ipm355 import QPSolver
-    # the batched plans keep the last block's own launch (no tail workgroup): the per-instance
-    # launches of the comparison run the same plan (IPM_TAIL=0)
-    monkeypatch.setenv("IPM_TAIL", "0")
-    zs = [_fixture(f"m4_qp_{sd}") for sd in range(1000, 1008)]
-    insts = [_instance(z)[1] for z in zs]
-    mk = lambda i: {k: v for k, v in insts[i].items()}   # noqa: E731
-    res = {}
-    for batch in (False, True):
-        sh = dist.Shard(mk, range(len(insts)), QPSolver, device=0, concurrent=True, batch=batch)
-        out = sh.solve()
-        res[batch] = (out, sh.xstar())
-        if batch:
-            launches, facts = sh.batch.stats()
-            print(f"[batched cholesky] {int(launches)} batched factorizations carrying {int(facts)} "
-                  f"({facts / max(launches, 1):.2f} per launch)")
-            assert facts > launches > 0
-    for i in range(len(insts)):
-        assert res[True][0][i][1] == res[False][0][i][1], i
-        np.testing.assert_array_equal(np.asarray(res[True][1][i]), np.asarray(res[False][1][i]))
-
-
 def test_sharded_two_ranks_real_solvers(tmp_path):
     """The sharded driver in TWO processes with the real device solver: launch_local
     starts 2 ranks (gloo: both share this box's GPU), each runs solve_sharded with QPSolver on its
