@@ -1170,11 +1170,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
 enum {
   CTL_TICKET = 0, CTL_PA_PROG = 1, CTL_PA_NEXT = 2, CTL_PB_PROG = 3, CTL_FAIL = 4,
   CTL_NF = 9,                         // next-diagonal-block fold tiles done
-  // critical-path roles (P(a) diagonal, the row chunks P(b) needs, the NF tiles, P(b) diagonal):
-  // CTL_CRIT + i holds 1 + the CU key while role i runs; CTL_SPILL + i a trailing tile handed off
-  // by a workgroup that landed on that CU
-  CTL_CRIT = 16, NCRIT = 16, CTL_SPILL = CTL_CRIT + NCRIT,
-  CTL_PB0 = CTL_SPILL + NCRIT,        // P(b)'s first row chunk done (the tail role waits for it)
+  CTL_PB0 = 16,                       // P(b)'s first row chunk done (the tail role waits for it)
   CTL_HDR = CTL_PB0 + 1
 };
 
@@ -1188,7 +1184,20 @@ enum {
 // next panel's diagonal block rows) and every chunk applies this panel to its rows of the next
 // panel's columns -- except the publishing chunks when fold_pub is false (the fused kernel folds
 // the next diagonal block with separate tile workgroups).
-template <bool FUSED = false>
+// LDS (VEC, IPM_ROW_LDS): the workgroup stages what its four waves share through LDS with 16-byte
+// direct loads (global_load_lds, sc1), all of it in flight at once: the off-diagonal L blocks and
+// Dinv of every block row the diagonal role has released (one memory latency when the role is
+// already done -- the row chunks of a trailing-bound launch start after its tiles -- instead of
+// one per block row), then per half of the fold its 128 x 64 operand and the destination values.
+// A chunk that starts after its diagonal role paid ~26 dependent memory latencies before
+// (profiles/r6rt: 33 us per P(a) chunk in the tail of launch 16 at n = 8192).  Every value is
+// formed by the same operations as the register path.  Off by default: measured slower
+// (profiles/r6x/ab3: n = 8193 5.59 -> 5.68 ms, 2048 0.600 -> 0.61 ms; the kernel's SGPR spills
+// 16 -> 55, and in chain-bound launches every block row adds a barrier round trip).
+#ifndef IPM_ROW_LDS
+#define IPM_ROW_LDS 0
+#endif
+template <bool FUSED = false, bool LDS = false>
 __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, int nb, double* __restrict__ A,
                                          int64_t lda, const double* dinv, const double* pubL,
                                          unsigned* progress, int next_nb, unsigned* nextc, double* stage,
@@ -1210,6 +1219,63 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
   dbl4 x[8];
 #pragma unroll
   for (int J = 0; J < 8; ++J) x[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+  if constexpr (LDS) {
+    // sL: off-diagonal block (J, P) at sL[(J (J - 1) / 2 + P) 256], Dinv_J at sL[7168 + 256 J]
+    // (9216 doubles: the diagonal role's sD)
+    double* sL = stage;
+    const int nJ = (nb + 15) >> 4;
+    int issued = 0;   // block rows [0, issued) are in LDS (workgroup-uniform)
+#pragma unroll
+    for (int J = 0; J < 8; ++J) {
+      if (J >= nJ) break;
+      if (issued <= J) {
+        if (tid == 0) {
+          // (no bound of its own: see the register path below)
+          unsigned kn = ld_ctl(progress);
+          while (kn <= (unsigned)J) {
+            __builtin_amdgcn_s_sleep(2);
+            kn = ld_ctl(progress);
+          }
+          *sflag = (int)min(kn, 8u);   // 0xFFFFFFFF (failed diagonal): everything, on garbage
+        }
+        __syncthreads();
+        const int upto = min(__builtin_amdgcn_readfirstlane(*sflag), nJ);
+        // block row r: 2 r wave instructions of L blocks (1 KB each), then 2 of Dinv_r
+        int ins = 0;
+        for (int r = issued; r < upto; ++r)
+          for (int q = 0; q < 2 * r + 2; ++q, ++ins) {
+            if ((ins & 3) != wv) continue;
+            const bool lq = q < 2 * r;
+            const double* src = lq ? pubL + bidx(r, q >> 1) * 256 + (q & 1) * 128 : dinv + r * 256 + (q - 2 * r) * 128;
+            double* dst = lq ? sL + ((r * (r - 1)) / 2 + (q >> 1)) * 256 + (q & 1) * 128
+                             : sL + 7168 + r * 256 + (q - 2 * r) * 128;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * lane),
+                                             (__attribute__((address_space(3))) void*)dst, 16, 0, 16);   // sc1
+          }
+        issued = upto;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      dbl4 acc = dbl4{b[J][0], b[J][1], b[J][2], b[J][3]};
+#pragma unroll
+      for (int P = 0; P < J; ++P) {
+        const double* lb = sL + ((J * (J - 1)) / 2 + P) * 256 + fk * 16 + fr;
+        double av[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) av[s4] = -lb[64 * s4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], x[P][s4], acc, 0, 0, 0);
+      }
+      const double* ib = sL + 7168 + J * 256 + fk * 16 + fr;
+      double dvv[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) dvv[s4] = ib[64 * s4];
+      dbl4 xj = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(dvv[s4], acc[s4], xj, 0, 0, 0);
+      x[J] = xj;
+    }
+  } else {
   unsigned known = 0;
 #pragma unroll
   for (int J = 0; J < 8; ++J) {
@@ -1241,6 +1307,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
     for (int s4 = 0; s4 < 4; ++s4) xj = __builtin_amdgcn_mfma_f64_16x16x4f64(dvv[s4], acc[s4], xj, 0, 0, 0);
     x[J] = xj;
   }
+  }   // LDS
   // rows of the next panel's diagonal block are handed to the other workgroups of this launch
   const int nchd = (next_nb + PF_RB - 1) / PF_RB;
   const bool pub = chunk < nchd;
@@ -1284,6 +1351,53 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
   }
   __syncthreads();
   constexpr int SLAB = 128 * 16 + 16;   // one 16-row slab of the second factor, k-major (+ bank pad)
+  if constexpr (LDS) {
+    // per half h: the 4 slabs (16 columns each) as 64 wave instructions of 8 k rows x 16 columns,
+    // and the 16 destination values of this lane, all in flight before one wait
+    const bool go = *sflag != 0;
+#pragma unroll 1
+    for (int h = 0; h < 2 && go; ++h) {
+      if (64 * h >= next_nb) break;
+      __syncthreads();   // (h = 0: the TRSM's LDS reads and *sflag are done; h = 1: the last half's)
+      for (int i = wv; i < 64; i += 4) {
+        const int jl = i >> 4, kk = (i & 15) * 8 + (lane >> 3), jp = 16 * jl + 2 * (lane & 7);
+        if (64 * h + jp < next_nb) {
+          const double* src = A + (k0 + kk) * lda + k0 + nb + 64 * h + jp;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)(stage + jl * SLAB + (i & 15) * 128),
+                                           16, 0, 16);   // sc1
+        }
+      }
+      double cv[4][4];
+#pragma unroll
+      for (int jl = 0; jl < 4; ++jl)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 64 * h + 16 * jl + fk + 4 * r;
+          cv[jl][r] = (rfold && c < next_nb) ? ld_sc1(&A[(k0 + nb + c) * lda + row]) : 0.0;
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#pragma unroll
+      for (int jl = 0; jl < 4; ++jl) {
+        const int jt = 4 * h + jl;
+        if (16 * jt >= next_nb) break;
+        const int64_t col0 = k0 + nb + 16 * jt;
+        dbl4 acc = dbl4{cv[jl][0], cv[jl][1], cv[jl][2], cv[jl][3]};
+        const double* sb = stage + jl * SLAB + fk * 16 + fr;
+#pragma unroll
+        for (int P = 0; P < 8; ++P)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-sb[(16 * P + 4 * s4) * 16], x[P][s4], acc, 0, 0, 0);
+        if (rfold) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (16 * jt + fk + 4 * r < next_nb) st_sc1(&A[(col0 + fk + 4 * r) * lda + row], acc[r]);
+        }
+      }
+    }
+  } else {
 #pragma unroll 1
   for (int h = 0; h < 2 && *sflag; ++h) {
     if (64 * h >= next_nb) break;
@@ -1330,6 +1444,7 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
       }
     }
   }
+  }   // LDS
   }   // next_nb > 0
   if (done) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1610,20 +1725,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
       }
     }
   }
-  // critical-path role index (-1: none): keeps trailing tiles off this CU while it runs
-  int crit = -1;
-  if (kind == K_DIAG) crit = pb ? NCRIT - 1 : 0;
-  else if (kind == K_ROW && !pb && chunk < nchd) crit = 1 + (int)chunk;
-  else if (kind == K_NF && fwait) crit = 1 + nchd + (int)t;
-  if (crit >= NCRIT - 1 && !(kind == K_DIAG && pb)) crit = -1;   // (table full: not tracked)
-  if (crit >= 0 && tid == 0)
-    __hip_atomic_store(&b.ctl[CTL_CRIT + crit], 1u + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  struct CritEnd {   // clears the entry when the role returns
-    unsigned* w;
-    __device__ ~CritEnd() {
-      if (w && threadIdx.x == 0) __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  } crit_end{crit >= 0 ? &b.ctl[CTL_CRIT + crit] : nullptr};
   double* ws = pb ? b.wsB : b.wsA;
   unsigned* prog = &b.ctl[pb ? CTL_PB_PROG : CTL_PA_PROG];
   const int64_t kp = pb ? k1 : b.cb;
@@ -1654,7 +1755,7 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
       const int64_t r0 = b.wa + chunk * PF_RB;
       wait_la(r0, std::min<int64_t>(r0 + PF_RB, b.n - b.cb) - 1);
     }
-    row_role<true>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
+    row_role<true, VEC && IPM_ROW_LDS>(chunk, b.n, kp, nbp, b.A, b.lda, ws, ws + PF_DINV, prog, pb ? 0 : b.wbw, &b.ctl[CTL_PA_NEXT],
                    sm.d.sD, &sflag, pb ? (chunk == 0 && b.ntail ? &b.ctl[CTL_PB0] : nullptr) : &pa_done[chunk], false,
                    b.info, failw, b.ntail && (b.tail_o - (kp + nbp)) / PF_RB == chunk);
     return;
@@ -1883,38 +1984,13 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   }
   if (kind == K_TILE) {
     ROLE(4);
-    // A trailing tile that lands on the CU of a running critical-path role hands its tile to
-    // that role's spill word and sleeps, keeping the slot so that no MFMA tile shares the CU with
-    // the chain.  Every tile workgroup, after its own tile, takes what is in the spill words; the
-    // sleeper, once the role is done, runs its tile itself if nobody took it.
-    if (tid == 0) {
-      const unsigned me = 1u + cu_key();
-      int q = -1;
-      for (int i = 0; i < NCRIT && q < 0 && !(b.xf & 8); ++i)
-        if (ld_ctl(&b.ctl[CTL_CRIT + i]) == me) q = i;
-      if (q >= 0) {
-        ROLE(7);
-        __hip_atomic_store(&b.ctl[CTL_SPILL + q], (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        spin_until<20>(b.info, failw, [&] { return ld_ctl(&b.ctl[CTL_CRIT + q]) != me; });
-        sflag = (int)__hip_atomic_exchange(&b.ctl[CTL_SPILL + q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        sflag = (int)(t + 1);
-      }
-    }
-    // own tile, then the spill words (one tile call site: the tile code is inlined once)
-#pragma nounroll
-    for (int q = -1; q < NCRIT; ++q) {
-      if (q >= 0 && tid == 0)
-        sflag = ld_ctl(&b.ctl[CTL_SPILL + q]) == 0u
-                    ? 0
-                    : (int)__hip_atomic_exchange(&b.ctl[CTL_SPILL + q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int v = sflag;
-      __syncthreads();
-      if (v) {
+    // (Until round 5 a tile that landed on the CU of a running critical-path role handed its tile
+    // to a spill word and slept, keeping the slot; the r6 A/B put that at +4 % on the n = 8193
+    // factorization -- the sleepers and the spilled tiles ran in the launch tails -- and it went.)
+    {
+        const int64_t st0 = t;
         // S ticket -> strip tile (pair launches), whole tile, or one K-half of a split tile
         // (pieces: upper half, then lower)
-        const int64_t st0 = v - 1;
         const bool strip = st0 < b.nstrip;
         const int64_t st = strip ? st0 : st0 - b.nstrip, u = strip ? -1 : st - b.s_full;
         const int sp = u < 0 ? 0 : ((u & 1) ? 2 : 1);
@@ -1938,7 +2014,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
             g, strip ? st + (st >= 1 ? 1 : 0) /* (tile (0, 1) lies above the diagonal) */
                      : b.f0 + (u < 0 ? st : b.s_full + p),
             sm.g128, sp, b.sscr + p * (128 * 128), b.sflag + p, -1, -1, b.info, failw);
-      }
     }
   }
 }

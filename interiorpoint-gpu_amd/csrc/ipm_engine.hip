@@ -870,12 +870,16 @@ void prep_linesearch_dirs(ipm_problem* pr, bool zero_scal = false) {
     if (qpP && pr->m <= 0) gemv_n(st, pr->n, pr->n, 1.0, d.P, d.ldp, pr->dx, 0.0, pr->Pdx);
     return;
   } else {
-    gemv_n(st, pr->R + pr->K, pr->n, 1.0, d.X, d.ldx, pr->dx, 0.0, pr->Cdx);
-    // dlhs: dense rows from X dx; diagonal cones a * dx ; drhs = c_i.dx (0 without c)
-    copy(st, pr->dlhs, pr->Cdx, pr->R);
+    // dlhs: dense rows from X dx; diagonal cones a * dx ; drhs = c_i.dx (0 without c).  The X dx
+    // rows go straight to dlhs and drhs (one launch; round 5 formed X dx in Cdx and copied both
+    // parts out: two device copies per Newton step, r6 trace)
+    if (d.has_cone_c) {
+      gemv_n2(st, pr->n, pr->dx, pr->R, d.X, d.ldx, pr->dlhs, pr->K, d.X + pr->R * d.ldx, d.ldx, pr->drhs);
+    } else {
+      gemv_n(st, pr->R, pr->n, 1.0, d.X, d.ldx, pr->dx, 0.0, pr->dlhs);
+      fill(st, pr->drhs, pr->K, 0.0);
+    }
     for (int64_t c = 0; c < d.Kd; ++c) mul(st, pr->n, d.Ad + c * pr->n, pr->dx, 1.0, pr->dlhs + pr->R + c * pr->n);
-    if (d.has_cone_c) copy(st, pr->drhs, pr->Cdx + pr->R, pr->K);
-    else fill(st, pr->drhs, pr->K, 0.0);
     if (pr->nbb > 0) dslacks_lin(st, pr->n, 0, nullptr, d.lb != nullptr, d.ub != nullptr, pr->dx, dsh, pr->ds + pr->K);
   }
   if (!pr->lp && !pr->ph1 && d.P) gemv_n(st, pr->n, pr->n, 1.0, d.P, d.ldp, pr->dx, 0.0, pr->Pdx);
