@@ -773,7 +773,16 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         const int c = c0 + 8 * h, i = I * 16 + r2, j = Jc * 16 + c;
         const double2 v = *reinterpret_cast<const double2*>(&sD[cb + c * 16 + r2]);
         double* dst = A + (k0 + j) * lda + k0 + i;
-        if (v2 && I > Jc && i + 1 < nb && j < nb) {
+        if (FUSED) {
+          // write-through (sc1): with a leading dimension that is not a whole number of 128-byte
+          // lines, the line holding the block's last rows also holds the first rows of the row
+          // chunk below, which other workgroups of this launch write and read (sc1); a plain store
+          // would keep that line, with their rows as they were, in this XCD's L2
+          if (j < nb) {
+            if (i < nb && (I > Jc || r2 >= c)) st_sc1(dst, v.x);
+            if (i + 1 < nb && (I > Jc || r2 + 1 >= c)) st_sc1(dst + 1, v.y);
+          }
+        } else if (v2 && I > Jc && i + 1 < nb && j < nb) {
           *reinterpret_cast<double2*>(dst) = v;
         } else if (j < nb) {
           if (i < nb && (I > Jc || r2 >= c)) dst[0] = v.x;
@@ -1318,9 +1327,11 @@ __device__ __forceinline__ void row_role(int64_t chunk, int64_t n, int64_t k0, i
       for (int r = 0; r < 4; ++r) {
         const int c = J * 16 + fk + 4 * r;
         if (c < nb) {
-          // (sc1_rows: the chunk holding the tail rows -- its rows are read inside this launch by
-          // the tail workgroup, possibly on another XCD: write-through like the published chunks)
-          if (pub || sc1_rows) st_sc1(&A[(k0 + c) * lda + row], x[J][r]);
+          // (FUSED: every row write-through, like the published chunks -- the tail workgroup reads
+          // the last rows inside this launch, and a plain store would keep the line shared with
+          // the neighbouring chunk's rows (an unaligned leading dimension) in this XCD's L2 with
+          // that chunk's rows as they were: r6, 4 of 12 runs of the bordered n = 8193 trajectory)
+          if (FUSED || pub || sc1_rows) st_sc1(&A[(k0 + c) * lda + row], x[J][r]);
           else A[(k0 + c) * lda + row] = x[J][r];
         }
       }

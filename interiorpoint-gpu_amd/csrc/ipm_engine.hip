@@ -136,8 +136,18 @@ void derive(ipm_problem* pr) {
     pr->Sbar = pr->S;
   }
   // room for one bordered row (N+1 rows): the Newton right-hand side rides through the Cholesky
-  pr->ldh = (pr->N + 1) + ((pr->N + 1) & 1);
+  // ... and a leading dimension of whole 128-byte lines: every 16-row block of a column of H is then
+  // one cache line, so no line holds rows of two Cholesky roles (a line shared by a role that
+  // stores and one that reads rows handed off inside the same launch could be served stale from an
+  // XCD's L2: r6 saw 4 of 12 runs of the bordered n = 8193 trajectory differ with ld = 8194).
+  // IPM_LDH_ALIGN (doubles; 2 = the round-5 layout) is a test knob, read per problem.
+  const char* ela = getenv("IPM_LDH_ALIGN");
+  const int64_t la = ela && atol(ela) >= 1 ? (int64_t)atol(ela) : 16;
+  pr->ldh = (pr->N + 1 + la - 1) / la * la;
 }
+
+// leading dimension of the p x p Schur complement: whole 128-byte lines (as H's, derive())
+static inline int64_t schur_ld(int64_t p) { return (p + 15) / 16 * 16; }
 
 // the Newton step's Cholesky (potrf_lower_fused on the problem's stream)
 static int potrf_step(ipm_problem* pr, hipStream_t st, int64_t n, double* H, int64_t ldh, int* info, double* ws,
@@ -201,7 +211,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   pr->piv = c.take<int64_t>(N);
   if (pr->eq) {
     pr->Ybuf = c.take<double>(N * p);
-    pr->Sbuf = c.take<double>((p + (p & 1)) * p);
+    pr->Sbuf = c.take<double>(schur_ld(p) * p);
     pr->Wp = c.take<double>(p);
     pr->ATv = c.take<double>(N);
     pr->ATdv = c.take<double>(N);
@@ -222,7 +232,7 @@ int64_t carve(ipm_problem* pr, char* base) {
   {
     int64_t lw = 0;
     if (!pr->lu && !pr->diag && !pr->eq) lw = lstsq_ws_doubles(N, 1);
-    if (pr->lsq && pr->eq && !pr->diag) lw = lstsq_ws_doubles(n, p) + lstsq_ws_doubles(p, 1) + p * (p + (p & 1));
+    if (pr->lsq && pr->eq && !pr->diag) lw = lstsq_ws_doubles(n, p) + lstsq_ws_doubles(p, 1) + p * schur_ld(p);
     if (pr->lsq && pr->diag && pr->eq) lw = lstsq_ws_doubles(p, 1);
     pr->lsw = lw > 0 ? c.take<double>(lw) : nullptr;
   }
@@ -507,7 +517,26 @@ extern "C" int ipm_potrf_partial(ipm_handle* h, int64_t n, int64_t ncols, double
     HIPCHK(h, hipMalloc((void**)&h->pws, potrf_ws_doubles(n) * sizeof(double)));
     h->pws_n = n;
   }
-  potrf_lower_fused(h->stream, n, H, ldh, h->dinfo, h->pws, ncols);
+  // the fused factorization hands rows between workgroups inside each launch; it is run on a
+  // matrix whose columns start on 128-byte lines (no line holds rows of two roles: the solver's
+  // own matrices are laid out that way).  Any other layout is factored in an aligned copy.
+  if ((ldh % 16) != 0 || (reinterpret_cast<uintptr_t>(H) & 127) != 0) {
+    const int64_t ld2 = (n + 15) / 16 * 16;
+    double* tmp = nullptr;
+    if (n > 0) {
+      HIPCHK(h, hipMallocAsync((void**)&tmp, (size_t)(ld2 * n) * sizeof(double), h->stream));
+      HIPCHK(h, hipMemcpy2DAsync(tmp, ld2 * sizeof(double), H, ldh * sizeof(double), n * sizeof(double), n,
+                                 hipMemcpyDeviceToDevice, h->stream));
+    }
+    potrf_lower_fused(h->stream, n, tmp, ld2, h->dinfo, h->pws, ncols);
+    if (n > 0) {
+      HIPCHK(h, hipMemcpy2DAsync(H, ldh * sizeof(double), tmp, ld2 * sizeof(double), n * sizeof(double), ncols,
+                                 hipMemcpyDeviceToDevice, h->stream));
+      HIPCHK(h, hipFreeAsync(tmp, h->stream));
+    }
+  } else {
+    potrf_lower_fused(h->stream, n, H, ldh, h->dinfo, h->pws, ncols);
+  }
   HIPCHK(h, hipMemcpyAsync(h->hbuf, h->dinfo, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int inf;
@@ -1078,7 +1107,7 @@ int direction_feasible(ipm_problem* pr, double t, const ipm_newton_opts* o) {
 int direction_infeasible_lstsq(ipm_problem* pr, const double* v) {
   const ipm_problem_desc& d = pr->d;
   hipStream_t st = S(pr);
-  const int64_t n = pr->n, p = pr->p, lds = p + (p & 1);
+  const int64_t n = pr->n, p = pr->p, lds = schur_ld(p);
   int rc = expand_full_inplace(pr, pr->H, n, pr->ldh);
   if (rc) return rc;
   // the problem's least-squares workspace: H's factor, S's factor, a p x p temporary
@@ -1127,8 +1156,8 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
   if (pr->diag) {
     assemble_hessian(pr, t, pr->s0, false);
     inv_eps(st, n, pr->hdiag, 0.0, pr->tmpn);  // Hi = 1/h
-    // S = A diag(Hi) A^T   (lower, column-major ld = p + (p&1))
-    const int64_t lds = p + (p & 1);
+    // S = A diag(Hi) A^T   (lower, column-major ld = schur_ld(p))
+    const int64_t lds = schur_ld(p);
     SyrkEpi e;
     syrk_lower(st, p, n, 1.0, d.AT, p, nullptr, 0, pr->tmpn, 0.0, pr->Sbuf, lds, e);
     double* lw = nullptr;
@@ -1166,7 +1195,7 @@ int direction_infeasible(ipm_problem* pr, const double* x, const double* v, doub
     return IPM_OK;
   }
   assemble_hessian(pr, t, pr->s0, o->use_psd_condition != 0);
-  const int64_t lds = p + (p & 1);
+  const int64_t lds = schur_ld(p);
   if (!pr->use_backup) {
     potrf_lower_fused(st, pr->N, pr->H, pr->ldh, pr->info, pr->pws);
     // Y = H^-1 A^T  (n x p row-major); hg = H^-1 g

@@ -302,7 +302,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
-          acc[tj][ti][r] = (i < a.ni && j < a.nj) ? a.C[j * a.ldc + i] : 0.0;
+          // (SC1OUT, the Cholesky's look-ahead tiles: the C tile is read sc1 as well -- a plain load
+          // would leave the line, rows of neighbouring roles included, in this XCD's L2 until the
+          // tile's sc1 stores drop it, and sc1 readers of those rows on the same XCD could be
+          // served from it: r6, an unaligned leading dimension)
+          acc[tj][ti][r] = (i < a.ni && j < a.nj) ? (SC1OUT ? ld_sc1(&a.C[j * a.ldc + i]) : a.C[j * a.ldc + i]) : 0.0;
         }
       }
   }

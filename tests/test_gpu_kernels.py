@@ -440,3 +440,25 @@ def test_potrf_not_pd_info_matches_lapack():
         ref = int(str(e).split("-th")[0].split()[-1])
     assert info == ref == k + 1, (info, ref)
     assert rc != 0
+
+
+@pytest.mark.parametrize("n,ncols,lda", [(2049, 2048, 2050), (4097, 4096, 4098), (1030, 1030, 1031)])
+def test_potrf_unaligned_ld_is_deterministic(n, ncols, lda):
+    """ipm_potrf_partial with a leading dimension that is not a whole number of 128-byte lines is
+    factored in an aligned copy (the fused kernel's in-launch hand-offs need line-aligned columns,
+    r6): repeated factorizations are bitwise equal to each other and to the aligned layout's."""
+    import torch
+    rng = np.random.default_rng(n)
+    M = rng.uniform(-0.5, 0.5, size=(n, n))
+    A = M @ M.T + n * np.eye(n)
+    outs = []
+    for ld in (lda, lda, lda, (n + 15) // 16 * 16):
+        buf = torch.zeros(n, ld, dtype=torch.float64, device="cuda")
+        buf[:, :n] = dev(A)
+        rc, info = potrf(buf, n, ld, ncols)
+        assert rc == 0 and info == 0
+        outs.append(np.tril(host(buf).T[:n, :ncols]))
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
+    Lr = np.linalg.cholesky(A[:ncols, :ncols])
+    assert np.linalg.norm(outs[0][:ncols] - Lr) <= 1e-12 * np.linalg.norm(Lr)

@@ -199,6 +199,30 @@ def test_m3_phase1_snapshots(timing):
         np.testing.assert_array_equal(np.load("/tmp/ipm_ph1_snap_t0.npy"), np.stack([out[10], out[30]]))
 
 
+def test_m3_phase1_trajectory_is_deterministic():
+    """Run to run, the bordered phase-1 trajectory (n = 8193) is bitwise the same.  The fused
+    Cholesky hands rows between workgroups inside each launch; on a matrix whose leading dimension
+    is not a whole number of 128-byte lines, a line can hold rows of two roles and a stale copy of
+    it in one XCD's L2 gives a wrong factor.  r6 measured, at the round-5 layout (ld 8194), 4 of 12
+    runs of this trajectory differing (up to 1.7e-4 at step 30, some falling to the least-squares
+    backup); the solver now pads H to ld 8208 (derive(), ipm_engine.hip) and the C-ABI factors any
+    other layout in an aligned copy."""
+    z = _fixture("m3_qp_ph1")
+    spec, kw = _instance(z)
+    K = int(z["k_steps"])
+    prev = None
+    for r in range(4):
+        s = _cls(spec)(check_cvxpy=False, suppress_print=True, **kw)
+        s.solve(iteration_budget=K)
+        xk = s.phase1_solver.x.cpu().numpy()
+        err = rel(xk, z["x_k"])
+        print(f"run {r}: x_K rel {err:.2e}")
+        assert err <= max(XSTAR_RTOL, 4 * float(z["sens_xk_rel"])), err
+        if prev is not None:
+            np.testing.assert_array_equal(xk, prev)
+        prev = xk
+
+
 @pytest.mark.parametrize("name", ["m2_qp", "m3_qp_ph1", "m3_qp_feas", "m3_lp"])
 def test_linesearch_flip_rate(name, monkeypatch):
     """The 64-candidate table line search against the reference-exact one (IPM_LINESEARCH=compare:
