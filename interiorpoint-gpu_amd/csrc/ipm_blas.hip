@@ -544,6 +544,7 @@ struct DiagSmem {
   double srinv[8 * 16];  // 1 / L_cc per diagonal block
   double sdinv[2 * 256];  // V & 2097152: Dinv_J from the leaf (row-major), double-buffered by J
   int fail;
+  int rd1;               // wave 1 holds its copy of leaf J's diagonal rows: J + 1 (see the leaf)
 };
 
 // FUSED: inside the one-launch-per-block factorisation (k_potrf_block): the panel was written by
@@ -587,6 +588,7 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
   // the diagonal chain is the critical path; its CU-mates are trailing-update tiles
   if (FUSED && IPM_DIAG_PRIO > 0) __builtin_amdgcn_s_setprio(IPM_DIAG_PRIO);
   if (tid == 0) fail = 0;
+  if (tid == 0) sm.rd1 = 0;
   STAMP();
   const int i0 = 2 * (tid & 63), jb = tid >> 6;
   if (nb == PF_NB && ((lda & 1) == 0) && ((k0 & 1) == 0)) {
@@ -899,6 +901,17 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
         else rowb[c] = bval ? sD[bb + c * 16 + rr] : 0.0;
         if (DL) rowb[c] = idg ? (c == rr ? 1.0 : 0.0) : rowb[c];
       }
+      // Wave 0 writes the factored diagonal rows back over db at the end of its sweep, and wave 1
+      // (a second leaf wave while more than four tiles are below, J <= 3) reads the unfactored
+      // ones from db at the start of its own, with no barrier between: wave 1 says when its copy
+      // has landed, and wave 0 waits for that before it overwrites db.  (r6: a trailing tile on
+      // the same CU -- LDS and issue contention -- delayed wave 1 past wave 0's sweep in ~2 % of
+      // the n = 8193 factorizations: tiles J+5.. and Dinv_3 swept from factored rows, silently
+      // wrong; the round-5 sleep beside critical roles had kept that CU free.)
+      if (wv == 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&sm.rd1, J + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       int bad = 0;
       double dvs[16];
       // V & 65536 (lean tail): the failure test is one sum of the 16 pivot factors dv (NaN for a
@@ -1002,7 +1015,12 @@ __device__ __forceinline__ void diag_role(int64_t k0, int nb, double* __restrict
       if ((V & 65536) && wv == 0) {
         // the diagonal rows as they are (the upper part of a diagonal block is never read: the
         // inverse, the write-back and the row roles use its lower part only) and the 16 pivot
-        // factors -- wave-uniform values -- from ONE lane: no per-lane selects
+        // factors -- wave-uniform values -- from ONE lane: no per-lane selects.  Not before wave 1
+        // (when it sweeps this leaf too) holds its copy of the unfactored rows (above).
+        if (nbt > 4 || (DL && nbt == 4)) {
+          while (__hip_atomic_load(&sm.rd1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < J + 1)
+            __builtin_amdgcn_s_sleep(1);
+        }
         if (lane < 16) {
 #pragma unroll
           for (int c = 0; c < 16; ++c) sD[db + c * 16 + rr] = row[c];   // column-major

@@ -462,3 +462,27 @@ def test_potrf_unaligned_ld_is_deterministic(n, ncols, lda):
         np.testing.assert_array_equal(o, outs[0])
     Lr = np.linalg.cholesky(A[:ncols, :ncols])
     assert np.linalg.norm(outs[0][:ncols] - Lr) <= 1e-12 * np.linalg.norm(Lr)
+
+
+@pytest.mark.parametrize("n,ncols,lda", [(8193, 8192, 8208), (8194, 8193, 8208)])
+def test_potrf_repeat_is_bitwise(n, ncols, lda):
+    """The fused factorization is deterministic by construction (fixed reduction orders, ticketed
+    roles): 40 factorizations of one matrix are bitwise equal.  The diagonal-role race fixed in r6
+    (wave 1 reading LDS rows wave 0 had already overwritten; scripts/race_check.py) showed here as
+    1-8 differing runs in 250 at these shapes."""
+    import torch
+    torch.manual_seed(0)
+    M = torch.rand(n, n, dtype=torch.float64, device="cuda") - 0.5
+    A = M @ M.T + n * torch.eye(n, dtype=torch.float64, device="cuda")
+    buf0 = torch.zeros(n, lda, dtype=torch.float64, device="cuda")
+    buf0[:, :n] = A
+    ref = None
+    for r in range(40):
+        H = buf0.clone()
+        rc, info = potrf(H, n, lda, ncols)
+        assert rc == 0 and info == 0
+        Lf = torch.tril(H[:, :n].T)[:, :ncols]
+        if ref is None:
+            ref = Lf.clone()
+        else:
+            assert torch.equal(Lf, ref), f"run {r} differs"

@@ -200,13 +200,12 @@ def test_m3_phase1_snapshots(timing):
 
 
 def test_m3_phase1_trajectory_is_deterministic():
-    """Run to run, the bordered phase-1 trajectory (n = 8193) is bitwise the same.  The fused
-    Cholesky hands rows between workgroups inside each launch; on a matrix whose leading dimension
-    is not a whole number of 128-byte lines, a line can hold rows of two roles and a stale copy of
-    it in one XCD's L2 gives a wrong factor.  r6 measured, at the round-5 layout (ld 8194), 4 of 12
-    runs of this trajectory differing (up to 1.7e-4 at step 30, some falling to the least-squares
-    backup); the solver now pads H to ld 8208 (derive(), ipm_engine.hip) and the C-ABI factors any
-    other layout in an aligned copy."""
+    """Run to run, the bordered phase-1 trajectory (n = 8193) is bitwise the same.  r6 found the
+    fused Cholesky's diagonal role racing with itself: wave 0 wrote the factored diagonal rows back
+    over the LDS copy that wave 1 (a second leaf wave) had yet to read when a trailing tile on the
+    same CU slowed wave 1 down -- 4 of 12 runs of this trajectory differed (up to 1.7e-4 at step
+    30, some falling to the least-squares backup) once round 6 stopped keeping that CU free.  Wave 1
+    now signals when its copy has landed (diag_role, ipm_blas.hip)."""
     z = _fixture("m3_qp_ph1")
     spec, kw = _instance(z)
     K = int(z["k_steps"])
