@@ -1538,7 +1538,6 @@ struct BlockArgs {
   // tail_K) to the corner and factors it
   int ntail = 0, tail_r = 0, tail_R = 0, tail_K = 0;
   int64_t tail_o = 0, tail_k0 = 0;
-  unsigned xf = 0;              // IPM_POTRF_X: experiment bits (A/B builds of one library)
 };
 // this workgroup's compute unit: XCC id, SE / SH / CU ids from HW_ID
 __device__ __forceinline__ unsigned cu_key() {
@@ -1645,7 +1644,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   const bool la_fold = VEC && t < b.nla32 && (b.la32.K % 128) == 0;
   if (t < b.nla && !la_fold) {
     ROLE(0);
-    if (b.xf & 1) __builtin_amdgcn_s_setprio(2);
     int64_t rb;
     if (t < b.nla32) {
       mfma_tile<32, false, VEC, 2, true>(b.la32, t, sm.g32);
@@ -1774,7 +1772,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   }
   if (kind == K_ROW) {
     ROLE(pb ? 6 : (chunk < nchd ? 2 : 5));
-    if (b.xf & 2) __builtin_amdgcn_s_setprio(2);
     if (pb) {
       // rows relative to k1 = P(a)'s row origin: the P(a) chunks holding them are done
       const int64_t r0 = b.wbw + chunk * PF_RB;
@@ -1791,7 +1788,6 @@ __device__ __forceinline__ void potrf_block_body(const BlockArgs& b, int64_t t, 
   }
   if (kind == K_NF) {
     ROLE(frole);
-    if (b.xf & 4) __builtin_amdgcn_s_setprio(2);
     // destination block D (rows / columns fo.., fni x fnj, lower) -= L L^T over the fnp source
     // column passes [fsrc + 128 p, fsrc + 128 p + 128): one 32 x 32 lower tile per workgroup,
     // 16 x 16 per wave.  NF: D = P(b)'s diagonal block, L = P(a)'s rows of it (published by the
@@ -2451,8 +2447,6 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
       b.trace = bk == tb;
     }
 #endif
-    static const unsigned xf = [] { const char* e = getenv("IPM_POTRF_X"); return e ? (unsigned)strtoul(e, nullptr, 0) : 0u; }();
-    b.xf = xf;
     b.nra = (int)cdiv(std::max<int64_t>(n - cb - b.wa, 0), PF_RB);
     b.nrb = b.wbw > 0 ? (int)cdiv(std::max<int64_t>(n - cb - wb, 0), PF_RB) : 0;
     {
