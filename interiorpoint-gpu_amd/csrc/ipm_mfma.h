@@ -26,6 +26,7 @@
 #include <mutex>
 #include <queue>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "ipm_common.h"
@@ -173,6 +174,11 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
   constexpr int BM = M::BM, BK = M::BK, LD = M::LD, PT = M::PT, TPR = M::TPR, TWI = M::TWI, TWJ = M::TWJ;
   IPM_TSTAMP(0);
   IPM_TSTAMPR(6);
+#ifdef IPM_TILE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 4096)   // [5] XCC id << 32 | HW_ID
+    ipm_tile_stamps[blockIdx.x * 8 + 5] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                          __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
   auto& sX = sm.sX;
   auto& sY = sm.sY;
   // ---- tile of this workgroup
@@ -439,6 +445,69 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
       __syncthreads();
     }
     IPM_TSTAMP(2);
+  } else if constexpr (LOOP == 2) {
+    // the KKT SYRK's loop (r6): the X fragments go from memory straight into the MFMA operand
+    // registers -- lane (fr, fk) of wave (wi, wj) holds X[k = 16 s + 4 kk + fk][I0 + 64 wi + 16 t +
+    // fr] -- and only Y is staged through LDS (half the LDS stores and fragment reads of LOOP 1).
+    // Each k-row's fragment is reloaded for the next slab right after its MFMAs are issued (one
+    // slab of prefetch in the same registers).  The weight and the sign are applied to the operand
+    // as LOOP 1 applies them at its LDS store: the same products, bitwise.  tools/dtv_lab.hip (r6):
+    // 4.36-4.43 -> 4.12 ms on the full 8192^2 x 2048 weighted grid, 2.57-2.62 -> 2.34 ms at
+    // 4096^2 x 4608 (both operands from memory: best 3.85 ms but +-5 % from run to run).
+    double fy[PT];
+    auto fload = [&](int64_t s) {
+      const double2* ys = reinterpret_cast<const double2*>(yp + s * ystep);
+#pragma unroll
+      for (int q = 0; q < PT / 2; ++q) {
+        const double2 v = ys[q];
+        fy[2 * q] = v.x;
+        fy[2 * q + 1] = v.y;
+      }
+    };
+    auto fstore = [&](int buf) {
+#pragma unroll
+      for (int q = 0; q < PT; ++q) sY[buf][sr * LD + sc + q] = fy[q];
+    };
+    const double* xq = a.X + (kbeg + fk) * a.ldx + I0 + wi * (BM / 2) + fr;
+    const double* wq = WEIGHT ? a.w + kbeg + fk : nullptr;
+    double xr[BK / 4][TWI], wk[BK / 4];
+    auto xload = [&](int64_t s, int kk) {
+      const double* p = xq + (s * BK + kk * 4) * a.ldx;
+#pragma unroll
+      for (int t = 0; t < TWI; ++t) xr[kk][t] = p[t * 16];
+      if (WEIGHT) wk[kk] = wq[s * BK + kk * 4];
+    };
+    fload(0);
+    fstore(0);
+    fload(nslab > 1 ? 1 : 0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) xload(0, kk);
+    __syncthreads();
+    IPM_TSTAMP(1);
+    for (int64_t s = 0; s < nslab; ++s) {
+      const int buf = (int)(s & 1);
+      const double* by = sY[buf];
+      fstore(buf ^ 1);
+      fload(std::min<int64_t>(s + 2, nslab - 1));
+      const int64_t sn = std::min<int64_t>(s + 1, nslab - 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double av[TWJ], bv[TWI];
+#pragma unroll
+        for (int t = 0; t < TWJ; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * (BM / WJ) + t * 16 + fr];
+#pragma unroll
+        for (int t = 0; t < TWI; ++t) bv[t] = (WEIGHT ? xr[kk][t] * wk[kk] : xr[kk][t]) * xsg;
+        xload(sn, kk);
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    IPM_TSTAMP(2);
   } else {
     if (nslab > 0) {
       gload(0);
@@ -583,7 +652,7 @@ __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a
   __shared__ MfSmem<BM_, WJ> sm;
   for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
     if (BM_ == 128 && VEC && WJ == 2 && tile_fast_ok<BM_>(a, Lw))
-      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, (BM_ == 128 && VEC && WJ == 2) ? 1 : 0>(a, Lw, sm);
+      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, (BM_ == 128 && VEC && WJ == 2) ? 2 : 0>(a, Lw, sm);
     else
       mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
   }
@@ -601,7 +670,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t 
   if (a.info && *a.info != 0) return;
   __shared__ MfSmem<BM_, 2> sm;
   const int64_t b = blockIdx.x;
-  constexpr int FL = (BM_ == 128 && VEC) ? 1 : 0;
+  constexpr int FL = (BM_ == 128 && VEC) ? 2 : 0;   // (the fast loop with X fragments from memory)
   if (b < s_full) {
     if (FL && tile_fast_ok<BM_>(a, b)) mfma_tile<BM_, WEIGHT, VEC, 2, false, true, FL>(a, b, sm);
     else mfma_tile<BM_, WEIGHT, VEC, 2, false, true>(a, b, sm);
@@ -654,7 +723,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
   __shared__ MfSmem<BM, 2> sm;
   __shared__ int slast;
   int64_t b = blockIdx.x;
-  constexpr int FL = VEC ? 1 : 0;
+  constexpr int FL = VEC ? 2 : 0;   // (the fast loop with X fragments from memory)
   // block order: pieces first (default) or whole tiles first
   bool whole;
   if (pieces_last) {
@@ -689,30 +758,81 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
   const int64_t I0 = bi * BM, J0 = bj * BM;
   const bool cinit = a.sub || a.accum || (a.beta == 1.0 && a.alpha == -1.0 && !a.P && !a.dvec);
   const double* base = sscr + ti * P * (int64_t)(BM * BM);
-  // column-major tile: consecutive threads take consecutive i (coalesced partial and C traffic)
-  for (int e = tid; e < BM * BM; e += 256) {
-    const int il = e & (BM - 1), jl = e / BM;
-    const int64_t i = I0 + il, j = J0 + jl;
-    if (i >= a.ni || j >= a.nj || (a.tri && i < j)) continue;
-    // all P partial loads in flight at once (P <= 16), then the fixed-order sum
-    double pv[16];
+  // column-major tile: consecutive threads take consecutive i (coalesced partial and C traffic).
+  // 4 elements per pass (8 with 4 pieces) with all their partial loads issued back to back (the partials come
+  // from other CUs' stores: a memory round trip each), then the fixed-order sums p = 0 .. P-1.  The
+  // piece count is a compile-time constant in the common plans (4 / 8 / 16): with a run-time bound
+  // every load sat in its own conditional block and the compiler waited for each one -- the fixup
+  // of a 16-piece tile took ~200 us (r6, tools/syrk_lab.hip).
+  auto fixup = [&](auto pc) {
+    constexpr int NP = decltype(pc)::value, U = NP >= 8 ? 4 : 8;
+    for (int e0 = tid; e0 < BM * BM; e0 += U * 256) {
+      // every load of the pass (the partials, and the P / C values the epilogue reads) before its
+      // first store: vmcnt counts loads and stores in issue order, so a load behind a store waits
+      // for the store too -- one element at a time, the fixup was store-latency-bound
+      double pv[U][NP], pp[U], cv[U];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) pv[q] = q < P ? ld_sc1(&base[q * (int64_t)(BM * BM) + e]) : 0.0;
-    double s = 0.0;
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-      if (q < P) s += pv[q];
-    double* cp = a.C + j * a.ldc + i;
-    if (cinit) {
-      *cp = *cp + s;
-    } else {
-      double v = a.alpha * s;
-      if (a.beta != 0.0) v += a.beta * (*cp);
-      if (a.P) v += a.tP * a.P[j * a.ldp + i];
-      if (a.dvec && i == j) v += a.dvec[i];
-      *cp = v;
+        for (int q = 0; q < NP; ++q) pv[u][q] = ld_sc1(&base[q * (int64_t)(BM * BM) + e0 + 256 * u]);
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        const int64_t i = I0 + (e & (BM - 1)), j = J0 + e / BM;
+        ok[u] = !(i >= a.ni || j >= a.nj || (a.tri && i < j));
+        pp[u] = (ok[u] && !cinit && a.P) ? a.P[j * a.ldp + i] : 0.0;
+        cv[u] = (ok[u] && (cinit || a.beta != 0.0)) ? a.C[j * a.ldc + i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int e = e0 + 256 * u;
+        const int64_t i = I0 + (e & (BM - 1)), j = J0 + e / BM;
+        double sum = 0.0;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) sum += pv[u][q];
+        double* cp = a.C + j * a.ldc + i;
+        if (cinit) {
+          *cp = cv[u] + sum;
+        } else {
+          double v = a.alpha * sum;
+          if (a.beta != 0.0) v += a.beta * cv[u];
+          if (a.P) v += a.tP * pp[u];
+          if (a.dvec && i == j) v += a.dvec[i];
+          *cp = v;
+        }
+      }
+    }
+  };
+  if (P == 16) fixup(std::integral_constant<int, 16>{});
+  else if (P == 8) fixup(std::integral_constant<int, 8>{});
+  else if (P == 4) fixup(std::integral_constant<int, 4>{});
+  else {
+    for (int e = tid; e < BM * BM; e += 256) {
+      const int il = e & (BM - 1), jl = e / BM;
+      const int64_t i = I0 + il, j = J0 + jl;
+      if (i >= a.ni || j >= a.nj || (a.tri && i < j)) continue;
+      double pv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pv[q] = q < P ? ld_sc1(&base[q * (int64_t)(BM * BM) + e]) : 0.0;
+      double sum = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q < P) sum += pv[q];
+      double* cp = a.C + j * a.ldc + i;
+      if (cinit) {
+        *cp = *cp + sum;
+      } else {
+        double v = a.alpha * sum;
+        if (a.beta != 0.0) v += a.beta * (*cp);
+        if (a.P) v += a.tP * a.P[j * a.ldp + i];
+        if (a.dvec && i == j) v += a.dvec[i];
+        *cp = v;
+      }
     }
   }
+  IPM_TSTAMPR(7);   // (lab stamps: the fixup's end replaces the piece's exit)
   // every piece of this tile has counted: the counter goes back to zero for the next launch
   if (tid == 0) __hip_atomic_store(&cnt[ti], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
