@@ -508,6 +508,41 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
       __syncthreads();
     }
     IPM_TSTAMP(2);
+  } else if constexpr (LOOP == 3) {
+    // both operands' fragments from memory straight into registers: no LDS, no barriers (each
+    // fragment is read by the two waves that share it; tools/dtv_lab.hip V3)
+    const double* xq = a.X + (kbeg + fk) * a.ldx + I0 + wi * (BM / 2) + fr;
+    const double* yq = a.Y + (kbeg + fk) * a.ldy + J0 + wj * (BM / WJ) + fr;
+    const double* wq = WEIGHT ? a.w + kbeg + fk : nullptr;
+    double xr[BK / 4][TWI], yr[BK / 4][TWJ], wk[BK / 4];
+    auto load = [&](int64_t s, int kk) {
+      const double* p = xq + (s * BK + kk * 4) * a.ldx;
+      const double* q = yq + (s * BK + kk * 4) * a.ldy;
+#pragma unroll
+      for (int t = 0; t < TWI; ++t) xr[kk][t] = p[t * 16];
+#pragma unroll
+      for (int t = 0; t < TWJ; ++t) yr[kk][t] = q[t * 16];
+      if (WEIGHT) wk[kk] = wq[s * BK + kk * 4];
+    };
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) load(0, kk);
+    for (int64_t s = 0; s < nslab; ++s) {
+      const int64_t sn = std::min<int64_t>(s + 1, nslab - 1);
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double av[TWJ], bv[TWI];
+#pragma unroll
+        for (int t = 0; t < TWJ; ++t) av[t] = yr[kk][t];
+#pragma unroll
+        for (int t = 0; t < TWI; ++t) bv[t] = (WEIGHT ? xr[kk][t] * wk[kk] : xr[kk][t]) * xsg;
+        load(sn, kk);
+#pragma unroll
+        for (int tj = 0; tj < TWJ; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TWI; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+    }
   } else {
     if (nslab > 0) {
       gload(0);
@@ -576,8 +611,29 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
     }
     return;
   }
+  // PRE (the GEMM / SYRK fast loops): the epilogue operands of a 16-column block (P, and C when
+  // beta != 0) are loaded for all its elements before the block's first store -- vmcnt counts loads
+  // and stores in issue order, so a load behind a store also waits for the store, and one element
+  // at a time the KKT epilogue was ~74 us of a ~510 us tile (r6, tools/syrk_lab.hip stamps)
+  constexpr bool PRE = LOOP >= 2;
 #pragma unroll
-  for (int tj = 0; tj < TWJ; ++tj)
+  for (int tj = 0; tj < TWJ; ++tj) {
+    double pp[TWI][4], pc[TWI][4];
+    if constexpr (PRE) {
+      if (!cinit && SPLIT != 1) {
+#pragma unroll
+        for (int ti = 0; ti < TWI; ++ti) {
+          const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t j = J0 + wj * (BM / WJ) + tj * 16 + fk + 4 * r;
+            const bool ok = i < a.ni && j < a.nj && (!a.tri || i >= j);
+            pp[ti][r] = (ok && a.P) ? a.P[j * a.ldp + i] : 0.0;
+            pc[ti][r] = (ok && a.beta != 0.0) ? a.C[j * a.ldc + i] : 0.0;
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int ti = 0; ti < TWI; ++ti) {
       const int64_t i = I0 + wi * (BM / 2) + ti * 16 + fr;
@@ -597,14 +653,15 @@ __device__ __forceinline__ void mfma_tile(const GemmArgs& a, int64_t Lw, MfSmem<
             double av = acc[tj][ti][r];
             if (SPLITADD && SPLIT == 2) av += ld_sc1(&part[(j - J0) * BM + (i - I0)]);
             double v = a.alpha * av;
-            if (a.beta != 0.0) v += a.beta * (*cp);
-            if (a.P) v += a.tP * a.P[j * a.ldp + i];
+            if (a.beta != 0.0) v += a.beta * (PRE ? pc[ti][r] : *cp);
+            if (a.P) v += a.tP * (PRE ? pp[ti][r] : a.P[j * a.ldp + i]);
             if (a.dvec && i == j) v += a.dvec[i];
             *cp = v;
           }
         }
       }
     }
+  }
   if (SPLIT == 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -646,13 +703,19 @@ __device__ __forceinline__ bool tile_fast_ok(const GemmArgs& a, int64_t Lw) {
   return (bi + 1) * BM <= a.ni && (bj + 1) * BM <= a.nj && (a.K % 16) == 0;
 }
 
+// the fast loop of the GEMM / SYRK kernels: 2 (X fragments from memory, Y through LDS; r6), 1 (both
+// through LDS), 3 (both from memory)
+#ifndef IPM_SYRK_LOOP
+#define IPM_SYRK_LOOP 2
+#endif
+
 template <int BM_, bool WEIGHT, bool VEC, int WJ = 2>
 __global__ __launch_bounds__(128 * WJ, 2 / (WJ / 2)) void k_mfma_gemm(GemmArgs a) {
   if (a.info && *a.info != 0) return;
   __shared__ MfSmem<BM_, WJ> sm;
   for (int64_t Lw = blockIdx.x; Lw < a.nblk; Lw += gridDim.x) {
     if (BM_ == 128 && VEC && WJ == 2 && tile_fast_ok<BM_>(a, Lw))
-      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, (BM_ == 128 && VEC && WJ == 2) ? 2 : 0>(a, Lw, sm);
+      mfma_tile<BM_, WEIGHT, VEC, WJ, false, false, (BM_ == 128 && VEC && WJ == 2) ? IPM_SYRK_LOOP : 0>(a, Lw, sm);
     else
       mfma_tile<BM_, WEIGHT, VEC, WJ>(a, Lw, sm);
   }
@@ -670,7 +733,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_split(GemmArgs a, int64_t 
   if (a.info && *a.info != 0) return;
   __shared__ MfSmem<BM_, 2> sm;
   const int64_t b = blockIdx.x;
-  constexpr int FL = (BM_ == 128 && VEC) ? 2 : 0;   // (the fast loop with X fragments from memory)
+  constexpr int FL = (BM_ == 128 && VEC) ? IPM_SYRK_LOOP : 0;
   if (b < s_full) {
     if (FL && tile_fast_ok<BM_>(a, b)) mfma_tile<BM_, WEIGHT, VEC, 2, false, true, FL>(a, b, sm);
     else mfma_tile<BM_, WEIGHT, VEC, 2, false, true>(a, b, sm);
@@ -723,7 +786,7 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
   __shared__ MfSmem<BM, 2> sm;
   __shared__ int slast;
   int64_t b = blockIdx.x;
-  constexpr int FL = VEC ? 2 : 0;   // (the fast loop with X fragments from memory)
+  constexpr int FL = VEC ? IPM_SYRK_LOOP : 0;
   // block order: pieces first (default) or whole tiles first
   bool whole;
   if (pieces_last) {
@@ -839,18 +902,21 @@ __global__ __launch_bounds__(256, 2) void k_mfma_gemm_streamk(GemmArgs a, int64_
 
 // stream-K plan for nt 128-tiles on `slots` slots: pieces per tile P (0: not worth it) and the
 // piece length Kp (whole 16-row slabs); the last piece of a tile may be shorter
-// IPM_STREAMK: 0 off (the K-halves split tail), 1 pieces first, 2 pieces last,
-// 3 pieces first with at most 8 pieces per tile (default from two rounds of tiles up: 2.37 -> 2.30
-// ms at n = 8192, K = 2048, 2.63 -> 2.51 ms at n = 8100, K = 2050; profiles/r2_streamk_ab.txt);
-// a grid of one round and a remainder defaults to 2 (SOCP n = 4096, 528 tiles on 512 slots:
-// 1.51 -> 1.46 ms, profiles/r4q)
+// IPM_STREAMK: 0 off (the K-halves split tail), 1 pieces first, 2 pieces last (the default), 3
+// pieces first with at most 8 pieces per tile, 4 pieces last with at most 8.  Rounds 2-5 defaulted
+// to 3 from two rounds of tiles up (2.37 -> 2.30 ms at n = 8192, K = 2048; profiles/r2_streamk_ab.txt)
+// and to 2 below (SOCP n = 4096, 528 tiles on 512 slots: 1.51 -> 1.46 ms, profiles/r4q); with the
+// r6 tile loop and fixup, 2 is ahead at n = 8192 too (bench A/B: 2.200 vs 2.220 ms,
+// profiles/r6_syrk_lab/bench_ab_streamk.txt)
 inline int streamk_mode(int64_t nt = 0, int slots = 0) {
   static const int env = [] {
     const char* e = getenv("IPM_STREAMK");
     return e ? atoi(e) : -1;
   }();
   if (env >= 0) return env;
-  return (slots > 0 && nt < 2 * (int64_t)slots) ? 2 : 3;
+  (void)nt;
+  (void)slots;
+  return 2;
 }
 inline int streamk_plan(int64_t nt, int slots, int64_t cap, int64_t K, int64_t& q, int64_t& Kp) {
   const int mode = streamk_mode(nt, slots);
@@ -859,7 +925,7 @@ inline int streamk_plan(int64_t nt, int slots, int64_t cap, int64_t K, int64_t& 
   if (!mode || slots <= 0 || nt < slots) return 0;
   q = nt % slots;
   if (q == 0) return 0;
-  const int pmax = mode == 3 ? 8 : 16;
+  const int pmax = (mode == 3 || mode == 4) ? 8 : 16;
   int P = 1;
   while (P * 2 <= pmax && q * P * 2 <= slots && q * P * 2 <= cap && K / (P * 2) >= 64) P *= 2;
   if (P < 4) return 0;
@@ -960,7 +1026,7 @@ inline void mfma_gemm_launch_split(hipStream_t st, GemmArgs a, double* ws, int64
       unsigned* cnt = reinterpret_cast<unsigned*>(ws + cap * (int64_t)(128 * 128));
       if (!flags_zero) hipMemsetAsync(cnt, 0, qk * sizeof(unsigned), st);   // (per-piece words: never waited on)
       dim3 g((unsigned)(npc + s_full)), blk(256);
-      const int pl = streamk_mode(a.nblk, slots) == 2 ? 1 : 0;
+      const int pl = (streamk_mode(a.nblk, slots) == 2 || streamk_mode(a.nblk, slots) == 4) ? 1 : 0;
       if (a.w) {
         if (vec) hipLaunchKernelGGL((k_mfma_gemm_streamk<true, true>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
         else hipLaunchKernelGGL((k_mfma_gemm_streamk<true, false>), g, blk, 0, st, a, s_full, P, Kp, npc, ws, cnt, pl);
