@@ -12,13 +12,17 @@ EPS = np.finfo(np.float64).eps
 
 
 @pytest.mark.parametrize("k,n", [(4, 16), (1, 1), (16, 128), (37, 130), (300, 257), (512, 1024), (0, 5),
-                                 (2050, 700), (64, 1000), (2048, 8192), (2050, 8100), (600, 10000)])
+                                 (2050, 700), (64, 1000), (2048, 8192), (2050, 8100), (600, 10000),
+                                 (4608, 4096), (1024, 4096), (520, 4096), (300, 4096)])
 def test_syrk_weighted_matches_numpy(k, n):
     """Includes grids whose tail runs as split K halves (k_mfma_gemm_split: n = 1000 and 1024 on
     64-tiles -- every tile split, ragged edge tiles included) and as stream-K pieces
-    (k_mfma_gemm_streamk on 128-tiles, default IPM_STREAMK=3: n = 8192, K = 2048 -> 32 tail tiles
-    x 8 pieces; n = 8100, K = 2050 -> ragged edge tiles and a ragged last piece; n = 10000, K = 600
-    -> 3160 tiles, 88 tail tiles: too many for the 256 partial slots, so the K-halves split runs)."""
+    (k_mfma_gemm_streamk on 128-tiles, default IPM_STREAMK=2, pieces last: n = 8192, K = 2048 -> 32
+    tail tiles x 16 pieces; n = 8100, K = 2050 -> ragged edge tiles and 15 pieces, the run-time
+    piece count of the fixup; n = 10000, K = 600 -> 3160 tiles, 88 tail tiles: too many for the 256
+    partial slots, so the K-halves split runs).  n = 4096 (528 tiles on 512 slots, config 5's grid):
+    K = 4608 / 1024 -> 16 pieces, K = 520 -> 7 (run-time count), K = 300 -> 4: each compile-time
+    piece count of the fixup and the fallback."""
     rng = np.random.default_rng(k * 1000 + n)
     X = rng.uniform(-2, 2, (k, n))
     w = rng.uniform(0.1, 3, k)
