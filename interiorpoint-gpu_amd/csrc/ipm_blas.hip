@@ -2952,8 +2952,10 @@ __global__ __launch_bounds__(512, 1) void k_trinv128(int64_t n, const double* __
 // as those blocks are published, and holds the tile L_{B+1,B} in registers (thread (c, q): column
 // c, k-indices 32q .. 32q+31), all off the chain.  The chain step is then
 //   rhs = b_B - pre - L_{B+1,B}^T x_{B+1};   x_B = X_B rhs.
-// Hand-off as k_trsv_chain (sc1 stores, vmcnt(0), progress word; consumers poll and read with
-// sc1 loads).
+// Hand-off: sc1 stores of the x block; every consumer polls the x values it needs with sc1 loads
+// (y starts as TRSV_PENDING), the chain step and (r6) the pre sum alike.  The progress word is still
+// published (monotonic) but no longer waited on.  r6 hand-off lab (tools/handoff_lab.hip): one
+// store -> poll hop costs ~0.6 us, on one XCD or across XCDs alike.
 // -------------------------------------------------------------------------------------
 constexpr long long TRSV_PENDING = -1LL;   // 0xFFFF...F: y's content before its block is solved
 struct Trsv128Smem {
@@ -3004,7 +3006,11 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
     double acc[16];
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) acc[jj] = 0.0;
-    unsigned known = 0;
+    // (r6: each lane polls its two x values themselves -- y starts as TRSV_PENDING -- instead of
+    // waiting for the progress word of their ticket: the word is published after the y store, its
+    // wait, a barrier and an atomic, and the pre sum's last term (x_{B+2}) sat on the chain behind
+    // that extra round trip.  The same fma sequence: bitwise the same x.)
+    bool released = false;   // a poll ran out its bound: x is garbage, the error word says so
 #pragma nounroll
     for (int tp = 0; tp + 1 < t; ++tp) {
       const int64_t k0 = (int64_t)(nblk - 1 - tp) * TB2;
@@ -3018,14 +3024,18 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
         tv0[jj] = (cc < rows && kr < krows) ? src[0] : 0.0;
         tv1[jj] = (cc < rows && kr + 1 < krows) ? src[1] : 0.0;
       }
-      if (known <= (unsigned)tp) {
-        if (!spin_until<1, 1>(nullptr, nullptr, [&] { known = ld_ctl(&ctl[1]); return known > (unsigned)tp; })) {
-          __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          known = 0xFFFFFFFFu;   // (released: x is garbage, the error word says so)
-        }
+      double x0 = 0.0, x1 = 0.0;
+      auto landed = [&] {
+        x0 = kr < krows ? ld_sc1(y + k0 + kr) : 0.0;
+        x1 = kr + 1 < krows ? ld_sc1(y + k0 + kr + 1) : 0.0;
+        return __double_as_longlong(x0) != TRSV_PENDING && __double_as_longlong(x1) != TRSV_PENDING;
+      };
+      if (released) {
+        landed();
+      } else if (!spin_until<1, 1>(nullptr, nullptr, landed)) {
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        released = true;
       }
-      const double x0 = kr < krows ? ld_sc1(y + k0 + kr) : 0.0;
-      const double x1 = kr + 1 < krows ? ld_sc1(y + k0 + kr + 1) : 0.0;
 #pragma unroll
       for (int jj = 0; jj < 16; ++jj) acc[jj] = fma(tv1[jj], x1, fma(tv0[jj], x0, acc[jj]));
     }
