@@ -2957,7 +2957,18 @@ __global__ __launch_bounds__(512, 1) void k_trinv128(int64_t n, const double* __
 // published (monotonic) but no longer waited on.  r6 hand-off lab (tools/handoff_lab.hip): one
 // store -> poll hop costs ~0.6 us, on one XCD or across XCDs alike.
 // -------------------------------------------------------------------------------------
-constexpr long long TRSV_PENDING = -1LL;   // 0xFFFF...F: y's content before its block is solved
+constexpr long long TRSV_PENDING = -1LL;
+#ifdef IPM_ROLE_TRACE
+// backward-solve stamps of the last solve (trace builds): per ticket [0] pre sum done, [1] x_{B+1}
+// polled, [2] x_B stored (s_memrealtime)
+__device__ unsigned long long ipm_trsv_trace[512 * 4];
+extern "C" int ipm_debug_trsv_trace(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ipm_trsv_trace), sizeof(unsigned long long) * 4 * std::min(n, 512));
+}
+#define TRSV_STAMP(k) do { if (tid == 0 && t < 512) ipm_trsv_trace[4 * t + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TRSV_STAMP(k) do {} while (0)
+#endif   // 0xFFFF...F: y's content before its block is solved
 struct Trsv128Smem {
   double sX[TB2 * (TB2 + 1)];   // X_B, X[c][r] at r * 129 + c
   double sx[TB2];               // x_{B+1}
@@ -3069,6 +3080,7 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
       if ((lane & 3) == 0) sm.spre[16 * wv + col] = v1;
     }
     __syncthreads();
+    TRSV_STAMP(0);
     // ---- the chain step
     if (t > 0) {
       const int64_t k0 = r0 + TB2;
@@ -3091,6 +3103,7 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
         sm.sx[tid] = v;
       }
       __syncthreads();
+      TRSV_STAMP(1);
       double p = 0.0, p2 = 0.0;
 #pragma unroll
       for (int k = 0; k < 32; k += 2) {
@@ -3123,6 +3136,7 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
       st_sc1(y + r0 + c, (sm.spart[0][c] + sm.spart[1][c]) + (sm.spart[2][c] + sm.spart[3][c]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    TRSV_STAMP(2);
     // publish "tickets <= t solved": monotonic.  With the data-polled chain a later ticket can finish
     // (it only needs x_{B+1}, which it read from y) before this store lands; a plain store could
     // then move ctl[1] backwards and leave the pre loop above waiting forever.

@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(&ev, err, 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hy.data(), y, nstep * 8, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hx.data(), xcc, nstep * 4, hipMemcpyDeviceToHost));
-        if (ev || hy[nstep - 1] != (unsigned long long)(nstep - 1)) ok = false;
+        if (ev || hy[nstep - 1] != (unsigned long long)nstep) ok = false;   // (step k stores k + 1)
         for (int k = 1; k < nstep; ++k) same = same && ((hx[k] & 7) == (hx[0] & 7));
         if (rep >= 2) per.push_back((t[1] - t[0]) / 100.0 / (nstep - 1));
       }
