@@ -3081,6 +3081,11 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
     }
     __syncthreads();
     TRSV_STAMP(0);
+    // X_B's entries of this thread's second product (X[c][32q + k]) into registers before the chain
+    // step (r6: off the chain; the same fma sequence as reading them from LDS inside it)
+    double xrg[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) xrg[k] = sm.sX[(32 * q + k) * (TB2 + 1) + c];
     // ---- the chain step
     if (t > 0) {
       const int64_t k0 = r0 + TB2;
@@ -3119,13 +3124,12 @@ __global__ __launch_bounds__(512, 1) void k_trsv_bwd128(int64_t n, int nblk, con
     __syncthreads();
     {
       double p = 0.0, p2 = 0.0;
-      const double* xc = &sm.sX[32 * q * (TB2 + 1) + c];   // X[c][32q + k] at xc[k * 129]
 #pragma unroll
       for (int k = 0; k < 32; k += 2) {
-        p = fma(xc[k * (TB2 + 1)], sm.sv[32 * q + k], p);
-        p2 = fma(xc[(k + 1) * (TB2 + 1)], sm.sv[32 * q + k + 1], p2);
+        p = fma(xrg[k], sm.sv[32 * q + k], p);
+        p2 = fma(xrg[k + 1], sm.sv[32 * q + k + 1], p2);
       }
-      __syncthreads();
+      // (spart's last readers were the sv line above, before the barrier: no barrier needed here)
       sm.spart[q][c] = p + p2;
     }
     __syncthreads();
