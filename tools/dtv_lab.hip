@@ -304,6 +304,164 @@ __global__ __launch_bounds__(256, 2) void k_v4(ipm::GemmArgs a) {
   store_tile(a, I0, J0, wi, wj, fr, fk, acc);
 }
 
+// V6: V1 with the Y fragments of k-step kk + 1 read from LDS before k-step kk's MFMAs
+template <bool WEIGHT>
+__global__ __launch_bounds__(256, 2) void k_v6(ipm::GemmArgs a) {
+  __shared__ alignas(16) double sY[2][BK * LD];
+  const int64_t L = blockIdx.x, bi = L % a.tiles_i, bj = L / a.tiles_i;
+  const int64_t I0 = bi * BM, J0 = bj * BM;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv & 1, wj = wv >> 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int sr = tid / TPR, sc = (tid % TPR) * PT;
+  const int64_t nslab = a.K / BK;
+  const double* yp = a.Y + sr * a.ldy + J0 + sc;
+  const double* xq = a.X + (int64_t)fk * a.ldx + I0 + wi * 64 + fr;
+  const double* wq = a.w + fk;
+  double fy[PT];
+  auto fload = [&](int64_t s) {
+    const double2* ys = reinterpret_cast<const double2*>(yp + s * BK * a.ldy);
+#pragma unroll
+    for (int q = 0; q < PT / 2; ++q) {
+      const double2 v = ys[q];
+      fy[2 * q] = v.x;
+      fy[2 * q + 1] = v.y;
+    }
+  };
+  auto fstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < PT; ++q) sY[buf][sr * LD + sc + q] = fy[q];
+  };
+  double xr[4][TW], wk[4];
+  auto xload = [&](int64_t s, int kk) {
+    const double* p = xq + (s * BK + kk * 4) * a.ldx;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) xr[kk][t] = p[t * 16];
+    if (WEIGHT) wk[kk] = wq[s * BK + kk * 4];
+  };
+  dbl4 acc[TW][TW];
+#pragma unroll
+  for (int u = 0; u < TW; ++u)
+#pragma unroll
+    for (int v = 0; v < TW; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
+  fload(0);
+  fstore(0);
+  fload(nslab > 1 ? 1 : 0);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) xload(0, kk);
+  __syncthreads();
+  double av[2][TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) av[0][t] = sY[0][fk * LD + wj * 64 + t * 16 + fr];
+  for (int64_t s = 0; s < nslab; ++s) {
+    const int buf = (int)(s & 1);
+    const double* by = sY[buf];
+    fstore(buf ^ 1);
+    fload(std::min<int64_t>(s + 2, nslab - 1));
+    const int64_t sn = std::min<int64_t>(s + 1, nslab - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < 3) {
+#pragma unroll
+        for (int t = 0; t < TW; ++t) av[(kk + 1) & 1][t] = by[((kk + 1) * 4 + fk) * LD + wj * 64 + t * 16 + fr];
+      }
+      double bv[TW];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) bv[t] = WEIGHT ? xr[kk][t] * wk[kk] : xr[kk][t];
+      xload(sn, kk);
+#pragma unroll
+      for (int tj = 0; tj < TW; ++tj)
+#pragma unroll
+        for (int ti = 0; ti < TW; ++ti)
+          acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk & 1][tj], bv[ti], acc[tj][ti], 0, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TW; ++t) av[0][t] = sY[buf ^ 1][fk * LD + wj * 64 + t * 16 + fr];
+  }
+  store_tile(a, I0, J0, wi, wj, fr, fk, acc);
+}
+
+// V7: V1 with two slabs per barrier (four LDS buffers of Y: the stores of slabs s+2, s+3 and the
+// loads of s+4, s+5 once per pair)
+template <bool WEIGHT>
+__global__ __launch_bounds__(256, 2) void k_v7(ipm::GemmArgs a) {
+  __shared__ alignas(16) double sY[4][BK * LD];
+  const int64_t L = blockIdx.x, bi = L % a.tiles_i, bj = L / a.tiles_i;
+  const int64_t I0 = bi * BM, J0 = bj * BM;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv & 1, wj = wv >> 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int sr = tid / TPR, sc = (tid % TPR) * PT;
+  const int64_t nslab = a.K / BK;   // even
+  const double* yp = a.Y + sr * a.ldy + J0 + sc;
+  const double* xq = a.X + (int64_t)fk * a.ldx + I0 + wi * 64 + fr;
+  const double* wq = a.w + fk;
+  double fy[2][PT];
+  auto fload = [&](int64_t s, int h) {
+    const double2* ys = reinterpret_cast<const double2*>(yp + s * BK * a.ldy);
+#pragma unroll
+    for (int q = 0; q < PT / 2; ++q) {
+      const double2 v = ys[q];
+      fy[h][2 * q] = v.x;
+      fy[h][2 * q + 1] = v.y;
+    }
+  };
+  auto fstore = [&](int buf, int h) {
+#pragma unroll
+    for (int q = 0; q < PT; ++q) sY[buf][sr * LD + sc + q] = fy[h][q];
+  };
+  double xr[4][TW], wk[4];
+  auto xload = [&](int64_t s, int kk) {
+    const double* p = xq + (s * BK + kk * 4) * a.ldx;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) xr[kk][t] = p[t * 16];
+    if (WEIGHT) wk[kk] = wq[s * BK + kk * 4];
+  };
+  dbl4 acc[TW][TW];
+#pragma unroll
+  for (int u = 0; u < TW; ++u)
+#pragma unroll
+    for (int v = 0; v < TW; ++v) acc[u][v] = dbl4{0.0, 0.0, 0.0, 0.0};
+  fload(0, 0);
+  fload(1, 1);
+  fstore(0, 0);
+  fstore(1, 1);
+  fload(std::min<int64_t>(2, nslab - 1), 0);
+  fload(std::min<int64_t>(3, nslab - 1), 1);
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) xload(0, kk);
+  __syncthreads();
+  for (int64_t s = 0; s < nslab; s += 2) {
+    const int pb = (int)((s >> 1) & 1) * 2;   // buffers of this pair
+    fstore(pb ^ 2, 0);
+    fstore((pb ^ 2) + 1, 1);
+    fload(std::min<int64_t>(s + 4, nslab - 1), 0);
+    fload(std::min<int64_t>(s + 5, nslab - 1), 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double* by = sY[pb + h];
+      const int64_t sn = std::min<int64_t>(s + h + 1, nslab - 1);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        double av[TW], bv[TW];
+#pragma unroll
+        for (int t = 0; t < TW; ++t) av[t] = by[(kk * 4 + fk) * LD + wj * 64 + t * 16 + fr];
+#pragma unroll
+        for (int t = 0; t < TW; ++t) bv[t] = WEIGHT ? xr[kk][t] * wk[kk] : xr[kk][t];
+        xload(sn, kk);
+#pragma unroll
+        for (int tj = 0; tj < TW; ++tj)
+#pragma unroll
+          for (int ti = 0; ti < TW; ++ti)
+            acc[tj][ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[tj], bv[ti], acc[tj][ti], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  store_tile(a, I0, J0, wi, wj, fr, fk, acc);
+}
+
 // the Cholesky's trailing tiles: C -= X^T Y on a lower-triangle grid (LOOP 1 with / without the lazy
 // C read, LOOP 2)
 template <int LOOP, int LAZYC>
@@ -362,13 +520,11 @@ int main(int argc, char** argv) {
   };
   run(k_v0, "V0 library fast loop (weighted)", C0);
   run(k_v1<true>, "V1 X direct to registers (weighted)", C);
-  run(k_v2<true>, "V2 LDS both, fragment double buffer (weighted)", C);
-  run(k_v3<true>, "V3 both direct to registers, no LDS (weighted)", C);
-  run(k_v4<true>, "V4 V1 with two slabs of X prefetch (weighted)", C);
-  run(k_v0, "V0 again", C0);
+  run(k_v6<true>, "V6 V1 + Y fragments one k-step ahead", C);
+  run(k_v7<true>, "V7 V1 with two slabs per barrier", C);
   run(k_v1<true>, "V1 again", C);
-  run(k_v3<true>, "V3 again", C);
-  run(k_v4<true>, "V4 again", C);
+  run(k_v6<true>, "V6 again", C);
+  run(k_v7<true>, "V7 again", C);
   return 0;
 }
 
