@@ -490,3 +490,39 @@ def test_potrf_repeat_is_bitwise(n, ncols, lda):
             ref = Lf.clone()
         else:
             assert torch.equal(Lf, ref), f"run {r} differs"
+
+
+_STREAMK_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from gpu_util import colmajor_lower, syrk
+EPS = np.finfo(np.float64).eps
+worst = 0.0
+for k, n in [(2048, 4096), (520, 4096), (300, 4096)]:
+    rng = np.random.default_rng(k + n)
+    X = rng.uniform(-2, 2, (k, n))
+    w = rng.uniform(0.1, 3, k)
+    got = colmajor_lower(syrk(X, w, n), n)
+    ref = X.T @ (w[:, None] * X)
+    bound = 64 * EPS * (np.abs(X).T @ (w[:, None] * np.abs(X))) + 1e-300
+    worst = max(worst, float(np.max(np.tril(np.abs(got - ref) / bound))))
+print("worst", worst)
+"""
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4"])
+def test_syrk_streamk_modes(mode):
+    """Every IPM_STREAMK tail (0 K-halves, 1 / 2 pieces first / last, 3 / 4 the same with at most
+    8 pieces) on config 5's 528-tile grid at three K (16, 7 and 4 pieces in the default plan), each
+    in its own process (the knob is read once per process), within the 64 eps bound."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(here, "..", "interiorpoint-gpu_amd")
+    env = dict(os.environ, IPM_STREAMK=mode)
+    out = subprocess.run([sys.executable, "-c", _STREAMK_CHILD, here, pkg], env=env, capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    worst = float(out.stdout.split("worst")[-1])
+    assert worst <= 1.0, worst
