@@ -2234,9 +2234,13 @@ static void potrf_plan(int64_t n, double* A, int64_t lda, int* info, double* ws,
   const int64_t nblocks = cdiv(ncols, CH_NB), cw = block_ctl_words(n);
   unsigned* ctl0 = reinterpret_cast<unsigned*>(ws + 2 * PANEL_WS);
   const bool vec = ((lda & 1) == 0) && ((((uintptr_t)A) & 15) == 0);
-  // IPM_RAG=0: ragged trailing rows as a row of 128-tiles (read per call: tests compare both)
+  // IPM_RAG=0 / 1: ragged trailing rows as a row of 128-tiles / by the ragged-row workgroups (read
+  // per call: tests compare both).  Unset: the workgroups above 5120 rows only -- r6, one-box A/B
+  // (profiles/r6g/potrf_ragged_rows_ab.txt): the bordered sizes n = 2049 / 3073 / 4097 factor
+  // 0.673 / 1.105 / 1.69 -> 0.602 / 1.003 / 1.56 ms as tiles, n = 6145 / 8193 3.14 / 5.54-5.65 ->
+  // 3.18 / 5.81-5.83 ms
   const char* erag = getenv("IPM_RAG");
-  const bool rag_on = !(erag && erag[0] == '0');
+  const bool rag_on = erag ? erag[0] != '0' : n > 5120;
   // IPM_SPLIT=0: no K-split trailing tiles (read per call: tests compare both)
   const char* esp = getenv("IPM_SPLIT");
   const bool split_on = !(esp && esp[0] == '0');

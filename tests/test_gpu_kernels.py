@@ -132,7 +132,7 @@ def test_potrs_single_rhs_persistent_solve(n):
 @pytest.mark.parametrize("n,ncols", [(8194, 8193), (1030, 1030), (2690, 2689)])
 def test_potrf_ragged_rows(n, ncols, monkeypatch):
     """The 1-8 trailing rows past a multiple of 128 (the bordered Newton system) are updated by
-    row workgroups (IPM_RAG, default) instead of a row of 128-tiles: same factor to fp64 rounding
+    row workgroups (IPM_RAG=1; the default above 5120 rows) instead of a row of 128-tiles: same factor to fp64 rounding
     as the tile path, and torch's Cholesky / triangular solve to 1e-10."""
     import torch
     from gpu_util import potrf as P
